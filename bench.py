@@ -1,0 +1,245 @@
+#!/usr/bin/env python3
+"""bench.py -- full-search block matching throughput on MI355X.
+
+Metric (BASELINE.json): 16x16 SAD candidates/sec at 1080p +-32; achieved HBM
+GB/s vs roofline.  One step = one full search of a 1920x1080 Y-frame pair
+(B=16, S=32, SAD, 33,188,832 exact candidates) per rank, inputs resident in
+HBM before the timed region.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--mode frames|stripe]
+                  [--config 1080p|4k|8k] [--cost sad|ssd] [--no-cpu]
+
+--mode frames (default): each rank searches its own frame pair per step (a
+  sequence sharded across GPUs): weak scaling, no collective in the data path.
+--mode stripe: ONE frame per step split into candidate-balanced block-row
+  stripes, one per rank, each rank holding only its stripe + S-row ref halo;
+  the per-stripe MV records are gathered to rank 0 with one RCCL gather inside
+  the timed step (strong scaling).
+For N > 1 launch with torch.distributed.run (one process per GPU, RCCL).
+Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import subprocess
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "16×16 SAD candidates/sec at 1080p ±32; achieved HBM GB/s vs roofline"
+HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
+VALU_PEAK_ABSDIFF = 157.3e12  # 256 CU x 64 lanes x 2.4 GHz x 4 |a-b| per op (measured: profiles/)
+CONFIGS = {  # name -> (synth config, block, range)
+    "1080p": ("1080p", 16, 32),
+    "4k": ("4k", 16, 64),
+    "8k": ("8k", 8, 128),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--mode", choices=["frames", "stripe"], default="frames")
+    ap.add_argument("--config", choices=list(CONFIGS), default="1080p")
+    ap.add_argument("--cost", choices=["sad", "ssd"], default="sad")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    return ap.parse_args()
+
+
+def cpu_baselines(ref, cur, blk, span, cost, threads, cands):
+    """Rank 0, N=1 only: the oracle restatement (port) timed on the host cores
+    on the same frame pair, and the reference's own binary (oracle/_ref/mes,
+    MSE cost, its hard-coded 100-thread pool) when it was built."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_lib as O
+    times = []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        O.full_search(ref, cur, blk, span, cost, threads=threads)
+        times.append(time.perf_counter() - t0)
+    med = statistics.median(times)
+    out = {"value": cands / med, "unit": "candidates/s", "cores": threads, "kind": "port",
+           "sample": f"the full {ref.shape[1]}x{ref.shape[0]} B{blk} +-{span} {cost.upper()} frame, "
+                     f"oracle/me_oracle.c -O2, {threads} pthreads, median of 5 ({med*1e3:.1f} ms)"}
+    mes = os.path.join(REPO, "oracle", "_ref", "mes")
+    if os.path.exists(mes):
+        with tempfile.TemporaryDirectory() as td:
+            rp, cp = os.path.join(td, "ref.yuv"), os.path.join(td, "cur.yuv")
+            ref.tofile(rp)
+            cur.tofile(cp)
+            ms = []
+            for _ in range(3):
+                r = subprocess.run([mes, cp, rp, td, str(blk), str(span), str(ref.shape[1]),
+                                    str(ref.shape[0])], capture_output=True, text=True, timeout=300)
+                for line in r.stdout.splitlines():
+                    if line.startswith("Computation time:"):
+                        ms.append(float(line.split()[2]))
+            if ms:
+                m = statistics.median(ms)
+                out["reference_binary"] = {
+                    "value": cands / (m / 1e3), "unit": "candidates/s", "cores": 100,
+                    "kind": "reference", "cost": "mse",
+                    "sample": f"unmodified src/cpu (gcc -O2) on the same frame pair, its own "
+                              f"100-thread pool, 'Computation time' median of 3 ({m:.0f} ms)"}
+    return out
+
+
+def load_traffic(tag):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary of this
+    workload (tools/profile.sh), or None."""
+    path = os.path.join(REPO, "profiles", "pmc_summary.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get(tag, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and world > 1:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    import motionestimation_amd as me
+    from motionestimation_amd import shard, synth
+
+    cfg, blk, span = CONFIGS[args.config]
+    w, h, seed, sx, sy = synth.CONFIGS[cfg]
+    cands_frame = me.candidate_count(w, h, blk, span)
+    nb = me.num_blocks(w, h, blk)
+    eng = me.Engine(devices=[local])
+
+    if args.mode == "frames":
+        # rank r: its own frame pair of the sequence (same size; seed varies)
+        ref, cur = synth.frame_pair(w, h, seed + rank, sx, sy)
+        ref_t = torch.from_numpy(ref).to(dev)
+        cur_t = torch.from_numpy(cur).to(dev)
+        mv_t = torch.empty((nb, 2), dtype=torch.int16, device=dev)
+        cost_t = torch.empty(nb, dtype=torch.int32, device=dev)
+
+        def step():
+            eng.full_search_device(ref_t, cur_t, blk, span, args.cost, mv_t, cost_t)
+        units_per_step = cands_frame * world
+    else:
+        ref, cur = synth.frame_pair(w, h, seed, sx, sy)
+        stripes = shard.plan(w, h, blk, span, world)
+        st = stripes[rank]
+        ref_t = torch.from_numpy(ref[st.ref_y0:st.ref_y1].copy()).to(dev)
+        cur_t = torch.from_numpy(cur[st.cur_y0:st.cur_y1].copy()).to(dev)
+        rec = torch.zeros((2, st.max_blocks), dtype=torch.int32, device=dev)
+        mv_view = rec[0].view(torch.int16).view(st.max_blocks, 2)
+        cost_view = rec[1]
+        bufs = [torch.empty_like(rec) for _ in range(world)] if rank == 0 else None
+
+        def step():
+            if st.nblocks:
+                eng.search_stripe_device(ref_t, st.ref_y0, cur_t, st.cur_y0, w, h, blk, span,
+                                         args.cost, st.row_begin, st.row_end, mv_view, cost_view)
+            if world > 1:
+                dist.gather(rec, bufs, dst=0)
+        units_per_step = cands_frame
+
+    # warmup (untimed)
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    # kernel duration: HIP events on the stream the search is launched on
+    # (torch's current stream), one pair per step, averaged.
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        evs[i][0].record()
+        step()
+        evs[i][1].record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = statistics.mean(a.elapsed_time(b) for a, b in evs)
+    if world > 1:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+
+    value = units_per_step * args.steps / elapsed
+    # Roofline of the dominant kernel: algorithmic HBM bytes per
+    # launch = 2*W*H (u8 ref + cur, read once) + 8*nblocks (mv + cost written)
+    # for the planes that launch covers.
+    if args.mode == "frames":
+        alg_bytes = 2 * w * h + 8 * nb
+        absdiffs = cands_frame * blk * blk
+    else:
+        alg_bytes = (st.ref_y1 - st.ref_y0 + st.cur_y1 - st.cur_y0) * w + 8 * st.nblocks
+        absdiffs = cands_frame * blk * blk / world
+    achieved = alg_bytes / (kern_ms / 1e3) / 1e9
+    tag = f"{args.config}_b{blk}_s{span}_{args.cost}"
+    traffic = load_traffic(tag)
+    line = {
+        "metric": METRIC if args.config == "1080p" and args.cost == "sad" else
+        f"{blk}x{blk} {args.cost.upper()} candidates/sec at {args.config} +-{span}",
+        "value": value,
+        "unit": "candidates/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak" if args.mode == "frames" else "strong",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": f"synthetic: motionestimation_amd.synth '{cfg}' (splitmix64 seed {seed}"
+                f"{'+rank' if args.mode == 'frames' else ''}, 5x5 box, cur = ref shifted "
+                f"({sx:+d},{sy:+d}) + uniform [-2,2])",
+        "config": {"workload": f"{w}x{h} Y, {blk}x{blk} blocks, full search +-{span}, "
+                               f"{args.cost.upper()}, {'one frame pair per rank per step' if args.mode == 'frames' else 'one frame per step in row stripes + RCCL gather'}",
+                   "width": w, "height": h, "block": blk, "range": span, "cost": args.cost,
+                   "candidates_per_frame": cands_frame, "blocks_per_frame": nb,
+                   "parallelism": f"{args.mode}{world}"},
+        "kernel_ms": kern_ms,
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "algorithmic_bytes_per_launch": alg_bytes,
+                     "valu": {"achieved_absdiff_per_s": absdiffs / (kern_ms / 1e3),
+                              "peak_absdiff_per_s": VALU_PEAK_ABSDIFF,
+                              "frac": absdiffs / (kern_ms / 1e3) / VALU_PEAK_ABSDIFF}},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        line["cpu_baseline"] = cpu_baselines(ref, cur, blk, span, args.cost, args.cpu_threads,
+                                             cands_frame)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

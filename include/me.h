@@ -1,0 +1,165 @@
+/*
+ * me.h -- C ABI of the MI355X full-search block-matching engine (libme_hip.so).
+ *
+ * Drop-in boundary for the reference's hot path (souravBhat/MotionEstimation,
+ * paths relative to the reference tree):
+ *
+ *   reference seam                                   replaced by
+ *   -----------------------------------------------  ---------------------------------
+ *   dispatch region src/cpu/main.c:144-158           me_full_search()
+ *     (thpool_init(100) + one findBestBlkMse job       frame level, host planes,
+ *      per block + thpool_wait)                        synchronous
+ *   findBestBlkMse  src/cpu/main.c:67-82             me_full_search() / me_find_best_blocks()
+ *     + findBestMatchMse :39-64 + computeMse :18-36    (per-block calls make no sense on a GPU)
+ *   GPU host region src/gpu/main_mse.cu:202-229      me_full_search_device() (HBM-resident,
+ *     (H2D, f_findBestMatchBlock<<<>>>, D2H)           stream-ordered)
+ *   block list filled for motionCompensatedFrame     me_find_best_blocks() writes the
+ *     src/common/utils.c:102-108                       reference's block records
+ *
+ * Semantics (identical to src/cpu on the same inputs):
+ *   - blocks tile the frame in raster order, ceil(W/B) x ceil(H/B), partial
+ *     blocks on the right/bottom edges   (src/common/prediction_frame.c:9-23)
+ *   - candidates: every top-left whose whole block fits the window
+ *     [tl - S, br + S] clamped to the frame   (src/cpu/main.c:53-54, 73-76)
+ *   - the first minimum in raster order (y outer, x inner, strict <) wins
+ *     (src/cpu/main.c:53-60)
+ *   - MV = candidate top-left - block top-left   (src/cpu/main.c:58-59)
+ *   - ME_COST_SSD reproduces the reference's float-MSE choice bit for bit:
+ *     block_cost = integer SSD of the chosen vector and the reference's score
+ *     is (float)block_cost / (float)(w*h) for w*h <= 256; larger blocks are
+ *     searched with the reference's float accumulation replayed exactly.
+ *   - ME_COST_SAD: same loops and tie rule with |cur - ref| (the reference
+ *     has no SAD; parity is against the repo's CPU restatement).
+ *
+ * Conventions: host buffers are caller-owned; host entry points are
+ * synchronous on return.  A context is used by one host thread at a time.
+ * Errors are returned, never exit()ed (the reference exits: main.c:134-139).
+ */
+#ifndef ME_H
+#define ME_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ME_API_VERSION 1
+
+typedef enum {
+  ME_OK = 0,
+  ME_EINVAL = 1,      /* bad argument (sizes, null pointers, block/range limits) */
+  ME_ENOMEM = 2,      /* host or device allocation failed */
+  ME_EDEVICE = 3,     /* HIP runtime / kernel launch error */
+  ME_ECOMM = 4,       /* RCCL error in the multi-device gather */
+  ME_EUNSUPPORTED = 5 /* valid request this build cannot serve */
+} me_status;
+
+typedef enum {
+  ME_COST_SSD = 0, /* reference parity: float MSE argmin; cost = SSD */
+  ME_COST_SAD = 1  /* sum of absolute differences */
+} me_cost;
+
+/* Limits of this build. */
+#define ME_MAX_BLOCK 64    /* block_size in [1, 64]  (SSD of 64x64 < 2^32) */
+#define ME_MAX_RANGE 1024  /* search_range in [0, 1024] */
+
+typedef struct me_ctx me_ctx;
+
+/* Create a context on n_devices HIP devices (device_ids may be NULL with
+ * n_devices <= 1: the current device).  With n_devices > 1 every search is
+ * split into macroblock row stripes, one per device, and the per-stripe MV
+ * fields are gathered to device_ids[0] with one RCCL ncclGather.  A device id
+ * may repeat: repeated ids run their stripes one after another on that device
+ * and are gathered by device copies (exercises the stripe path on one GPU). */
+me_status me_create(me_ctx** ctx, const int* device_ids, int n_devices);
+void me_destroy(me_ctx* ctx);
+
+const char* me_status_str(me_status s);
+/* Detail of the last error on this context ("" if none). */
+const char* me_last_error(const me_ctx* ctx);
+/* Library version string, e.g. "me_hip 1 gfx950". */
+const char* me_version(void);
+
+/* Tiling helpers (src/common/prediction_frame.c:9-11). */
+int me_num_blocks(int width, int height, int block_size);
+/* Exact number of candidates the search evaluates (reference clamping). */
+uint64_t me_candidate_count(int width, int height, int block_size, int search_range);
+
+/* Frame-level search on host Y planes (8-bit, row pitch `stride` >= width).
+ * mv_xy: [nblocks][2] int16 (mvx, mvy), block_cost: [nblocks] (may be NULL). */
+me_status me_full_search(me_ctx* ctx, const uint8_t* ref, const uint8_t* cur,
+                         int width, int height, int stride, int block_size,
+                         int search_range, me_cost cost, int16_t* mv_xy,
+                         uint32_t* block_cost);
+
+/* Same search on HBM-resident planes of ctx's first device, enqueued on
+ * `stream` (a hipStream_t; NULL = the legacy default stream), asynchronous.
+ * d_mv_xy / d_block_cost are device arrays of nblocks entries. */
+me_status me_full_search_device(me_ctx* ctx, const uint8_t* d_ref,
+                                const uint8_t* d_cur, int width, int height,
+                                int stride, int block_size, int search_range,
+                                me_cost cost, int16_t* d_mv_xy,
+                                uint32_t* d_block_cost, void* stream);
+
+/* One row stripe: block rows [block_row_begin, block_row_end).  d_ref holds
+ * frame rows starting at ref_row0 and must cover
+ *   [max(0, block_row_begin*B - S), min(H, block_row_end*B + S)),
+ * d_cur holds frame rows starting at cur_row0 and must cover
+ *   [block_row_begin*B, min(H, block_row_end*B)).
+ * Outputs hold the stripe's blocks only, raster order.  This is the unit a
+ * multi-process (one rank per GPU) caller shards with. */
+me_status me_full_search_stripe_device(me_ctx* ctx, const uint8_t* d_ref,
+                                       int ref_row0, const uint8_t* d_cur,
+                                       int cur_row0, int width, int height,
+                                       int stride, int block_size,
+                                       int search_range, me_cost cost,
+                                       int block_row_begin, int block_row_end,
+                                       int16_t* d_mv_xy, uint32_t* d_block_cost,
+                                       void* stream);
+
+/* Balanced stripe plan: bounds[0..n_shards] block-row boundaries, each stripe
+ * carrying about the same exact candidate count. */
+me_status me_plan_stripes(int width, int height, int block_size,
+                          int search_range, int n_shards, int* bounds);
+
+/* Reference block record, field for field src/common/block.h:6-19 (44 B). */
+typedef struct me_ref_block {
+  int idx_x, idx_y;
+  int top_left_x, top_left_y;
+  int bottom_right_x, bottom_right_y;
+  int width, height;
+  int is_best_match_found;
+  int motion_vectorX, motion_vectorY;
+} me_ref_block;
+
+/* Adapter for the reference driver: takes its int-widened planes
+ * (src/common/utils.c:49-53), searches with ME_COST_SSD and fills
+ * motion_vectorX/Y and is_best_match_found = 1 of every block exactly as the
+ * thread-pool loop at src/cpu/main.c:144-158 does.  blks must hold the
+ * me_num_blocks() records createPredictionFrame produced. */
+me_status me_find_best_blocks(me_ctx* ctx, const int* ref_frame,
+                              const int* cur_frame, int width, int height,
+                              int block_size, int search_range,
+                              me_ref_block* blks, int num_blks);
+
+/* ---- consumers of the MV field (src/common/utils.c:94-164) on the GPU ---- */
+
+/* mc[p] = ref[p + mv(block of p)], host planes, synchronous. */
+me_status me_motion_compensate(me_ctx* ctx, const uint8_t* ref, int width,
+                               int height, int block_size, const int16_t* mv_xy,
+                               uint8_t* mc);
+
+/* The reference's 5-plane output [ref, cur, mc, |ref-cur|, |mc-cur|]
+ * (src/cpu/main.c:161-168) into out[5*W*H], plus the PSNR of mc vs cur with
+ * the reference's MAX = largest pixel rule (src/common/utils.c:137-164). */
+me_status me_compensate_planes(me_ctx* ctx, const uint8_t* ref,
+                               const uint8_t* cur, int width, int height,
+                               int block_size, const int16_t* mv_xy,
+                               uint8_t* out5, double* psnr);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ME_H */

@@ -1,0 +1,89 @@
+"""ctypes binding of libme_hip.so (include/me.h).  No fallback: if the HIP
+library is missing or fails to load, every entry point raises."""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(PKG)
+LIB_PATH = os.path.join(PKG, "lib", "libme_hip.so")
+CSRC = os.path.join(PKG, "csrc")
+
+ME_OK, ME_EINVAL, ME_ENOMEM, ME_EDEVICE, ME_ECOMM, ME_EUNSUPPORTED = range(6)
+ME_COST_SSD, ME_COST_SAD = 0, 1
+ME_MAX_BLOCK, ME_MAX_RANGE = 64, 1024
+
+# Every symbol include/me.h declares, with (restype, argtypes).
+_u8p = ctypes.c_void_p
+_SIGS = {
+    "me_create": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_int),
+                                 ctypes.c_int]),
+    "me_destroy": (None, [ctypes.c_void_p]),
+    "me_status_str": (ctypes.c_char_p, [ctypes.c_int]),
+    "me_last_error": (ctypes.c_char_p, [ctypes.c_void_p]),
+    "me_version": (ctypes.c_char_p, []),
+    "me_num_blocks": (ctypes.c_int, [ctypes.c_int] * 3),
+    "me_candidate_count": (ctypes.c_uint64, [ctypes.c_int] * 4),
+    "me_full_search": (ctypes.c_int, [ctypes.c_void_p, _u8p, _u8p] + [ctypes.c_int] * 6 +
+                       [ctypes.c_void_p, ctypes.c_void_p]),
+    "me_full_search_device": (ctypes.c_int, [ctypes.c_void_p, _u8p, _u8p] + [ctypes.c_int] * 6 +
+                              [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "me_full_search_stripe_device": (ctypes.c_int, [ctypes.c_void_p, _u8p, ctypes.c_int, _u8p,
+                                                    ctypes.c_int] + [ctypes.c_int] * 8 +
+                                     [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "me_plan_stripes": (ctypes.c_int, [ctypes.c_int] * 5 + [ctypes.POINTER(ctypes.c_int)]),
+    "me_find_best_blocks": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p] +
+                            [ctypes.c_int] * 4 + [ctypes.c_void_p, ctypes.c_int]),
+    "me_motion_compensate": (ctypes.c_int, [ctypes.c_void_p, _u8p] + [ctypes.c_int] * 3 +
+                             [ctypes.c_void_p, ctypes.c_void_p]),
+    "me_compensate_planes": (ctypes.c_int, [ctypes.c_void_p, _u8p, _u8p] + [ctypes.c_int] * 3 +
+                             [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)]),
+}
+
+
+class MEError(RuntimeError):
+    def __init__(self, status: int, detail: str = ""):
+        self.status = status
+        name = _names.get(status, f"status {status}")
+        super().__init__(f"{name}: {detail}" if detail else name)
+
+
+_names = {ME_EINVAL: "ME_EINVAL", ME_ENOMEM: "ME_ENOMEM", ME_EDEVICE: "ME_EDEVICE",
+          ME_ECOMM: "ME_ECOMM", ME_EUNSUPPORTED: "ME_EUNSUPPORTED"}
+
+_lib = None
+
+
+def build(force: bool = False) -> str:
+    """Compile libme_hip.so in-tree for gfx950 (hipcc cross-compiles without a GPU)."""
+    cmd = ["make", "-s", "-C", CSRC]
+    if force:
+        cmd.append("-B")
+    subprocess.run(cmd, check=True)
+    return LIB_PATH
+
+
+def lib():
+    """The loaded library; raises if it is absent (the product has no CPU path)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} is missing: build it with "
+                               "`python -c 'import __graft_entry__; __graft_entry__.build()'`")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(status: int, ctx=None) -> None:
+    if status != ME_OK:
+        detail = ""
+        if ctx:
+            detail = (lib().me_last_error(ctx) or b"").decode()
+        raise MEError(status, detail)

@@ -1,0 +1,482 @@
+// me_api.hip -- C ABI of libme_hip.so (declared in include/me.h).
+//
+// Host side of the engine: argument checking (status codes, never exit()),
+// device buffers owned by the context, the stripe planner, and the
+// multi-device path (row stripes + one RCCL ncclGather of the per-stripe MV
+// records to the first device).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <new>
+#include <vector>
+
+#include "me.h"
+#include "me_kernels.h"
+
+namespace {
+
+struct Dev {
+  int id = 0;
+  hipStream_t stream = nullptr;
+  uint8_t* ref = nullptr;  // frame (or stripe) planes, packed pitch = width
+  uint8_t* cur = nullptr;
+  size_t frame_cap = 0;
+  uint8_t* rec = nullptr;  // [mv int16 x2 | cost u32] x rec_cap blocks
+  size_t rec_cap = 0;
+  uint8_t* gather = nullptr;  // root only: n_shards * rec bytes
+  size_t gather_cap = 0;
+  unsigned long long* stats = nullptr;
+  uint8_t* out5 = nullptr;
+  size_t out_cap = 0;
+};
+
+}  // namespace
+
+struct me_ctx {
+  std::vector<Dev> devs;
+  bool distinct = true;
+  ncclComm_t* comms = nullptr;
+  char err[512] = {0};
+};
+
+namespace {
+
+me_status fail(me_ctx* c, me_status s, const char* fmt, ...) {
+  if (c) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(c->err, sizeof c->err, fmt, ap);
+    va_end(ap);
+  }
+  return s;
+}
+
+#define HIPCHK(ctx, x)                                                                 \
+  do {                                                                                 \
+    hipError_t e_ = (x);                                                               \
+    if (e_ != hipSuccess)                                                              \
+      return fail(ctx, ME_EDEVICE, "%s:%d %s: %s", __FILE__, __LINE__, #x,             \
+                  hipGetErrorString(e_));                                              \
+  } while (0)
+
+#define NCCLCHK(ctx, x)                                                                \
+  do {                                                                                 \
+    ncclResult_t r_ = (x);                                                             \
+    if (r_ != ncclSuccess)                                                             \
+      return fail(ctx, ME_ECOMM, "%s:%d %s: %s", __FILE__, __LINE__, #x,               \
+                  ncclGetErrorString(r_));                                             \
+  } while (0)
+
+me_status grow(me_ctx* c, void** p, size_t* cap, size_t need) {
+  if (*cap >= need && *p) return ME_OK;
+  if (*p) (void)hipFree(*p);
+  *p = nullptr;
+  *cap = 0;
+  if (hipMalloc(p, need) != hipSuccess) {
+    *p = nullptr;
+    return fail(c, ME_ENOMEM, "hipMalloc(%zu) failed", need);
+  }
+  *cap = need;
+  return ME_OK;
+}
+
+me_status check_args(me_ctx* c, const void* ref, const void* cur, int width, int height,
+                     int stride, int blk, int range, int cost, const void* mv) {
+  if (!c) return ME_EINVAL;
+  if (!ref || !cur || !mv) return fail(c, ME_EINVAL, "null plane or output pointer");
+  if (width <= 0 || height <= 0) return fail(c, ME_EINVAL, "frame %dx%d", width, height);
+  if (stride < width) return fail(c, ME_EINVAL, "stride %d < width %d", stride, width);
+  if (blk < 1 || blk > ME_MAX_BLOCK) return fail(c, ME_EINVAL, "block_size %d", blk);
+  if (range < 0 || range > ME_MAX_RANGE) return fail(c, ME_EINVAL, "search_range %d", range);
+  if (cost != ME_COST_SSD && cost != ME_COST_SAD) return fail(c, ME_EINVAL, "cost %d", cost);
+  return ME_OK;
+}
+
+me::SearchArgs make_args(const uint8_t* ref, int ref_row0, const uint8_t* cur, int cur_row0,
+                         int width, int height, int stride, int blk, int range, int cost,
+                         int r0, int r1, int16_t* mv, uint32_t* cst) {
+  me::SearchArgs p;
+  p.ref = ref;
+  p.cur = cur;
+  p.ref_row0 = ref_row0;
+  p.cur_row0 = cur_row0;
+  p.width = width;
+  p.height = height;
+  p.stride = stride;
+  p.blk = blk;
+  p.range = range;
+  p.nbx = (width + blk - 1) / blk;
+  p.block_row_begin = r0;
+  p.block_row_end = r1;
+  p.cost_kind = cost;
+  p.mv = mv;
+  p.cost = cst;
+  return p;
+}
+
+uint64_t row_candidates(int width, int height, int blk, int range, int by) {
+  const int nbx = (width + blk - 1) / blk;
+  const int tly = by * blk;
+  const int h = height - tly < blk ? height - tly : blk;
+  const int dymin = -range > -tly ? -range : -tly;
+  const int dymax = range < height - h - tly ? range : height - h - tly;
+  uint64_t ny = (uint64_t)(dymax - dymin + 1), total = 0;
+  for (int bx = 0; bx < nbx; bx++) {
+    const int tlx = bx * blk;
+    const int w = width - tlx < blk ? width - tlx : blk;
+    const int dxmin = -range > -tlx ? -range : -tlx;
+    const int dxmax = range < width - w - tlx ? range : width - w - tlx;
+    total += (uint64_t)(dxmax - dxmin + 1) * ny;
+  }
+  return total;
+}
+
+me_status ensure_comms(me_ctx* c) {
+  if (c->comms || !c->distinct || c->devs.size() < 2) return ME_OK;
+  const int n = (int)c->devs.size();
+  std::vector<int> ids(n);
+  for (int i = 0; i < n; i++) ids[i] = c->devs[i].id;
+  c->comms = new (std::nothrow) ncclComm_t[n];
+  if (!c->comms) return fail(c, ME_ENOMEM, "comm array");
+  ncclResult_t r = ncclCommInitAll(c->comms, n, ids.data());
+  if (r != ncclSuccess) {
+    delete[] c->comms;
+    c->comms = nullptr;
+    return fail(c, ME_ECOMM, "ncclCommInitAll: %s", ncclGetErrorString(r));
+  }
+  return ME_OK;
+}
+
+// Multi-device frame search: row stripes, one per context device, then one
+// gather of the padded per-stripe record arrays to device 0.
+me_status multi_search(me_ctx* c, const uint8_t* ref, const uint8_t* cur, int width,
+                       int height, int stride, int blk, int range, int cost, int16_t* mv_xy,
+                       uint32_t* block_cost) {
+  const int n = (int)c->devs.size();
+  const int nby = (height + blk - 1) / blk, nbx = (width + blk - 1) / blk;
+  std::vector<int> bounds(n + 1);
+  me_status s = me_plan_stripes(width, height, blk, range, n, bounds.data());
+  if (s != ME_OK) return fail(c, s, "stripe plan");
+  int max_rows = 0;
+  for (int i = 0; i < n; i++)
+    max_rows = bounds[i + 1] - bounds[i] > max_rows ? bounds[i + 1] - bounds[i] : max_rows;
+  const size_t max_blocks = (size_t)(max_rows > 0 ? max_rows : 1) * nbx;
+  const size_t rec_bytes = max_blocks * 8;
+
+  for (int i = 0; i < n; i++) {
+    Dev& d = c->devs[i];
+    HIPCHK(c, hipSetDevice(d.id));
+    const int r0 = bounds[i], r1 = bounds[i + 1];
+    const int y_ref0 = r0 * blk - range > 0 ? r0 * blk - range : 0;
+    const int y_ref1 = r1 * blk + range < height ? r1 * blk + range : height;
+    const int y_cur0 = r0 * blk;
+    const int y_cur1 = r1 * blk < height ? r1 * blk : height;
+    const size_t ref_rows = r1 > r0 ? (size_t)(y_ref1 - y_ref0) : 0;
+    const size_t cur_rows = r1 > r0 ? (size_t)(y_cur1 - y_cur0) : 0;
+    if ((s = grow(c, (void**)&d.ref, &d.frame_cap, (ref_rows + cur_rows + 1) * width)) != ME_OK)
+      return s;
+    d.cur = d.ref + ref_rows * width;
+    if ((s = grow(c, (void**)&d.rec, &d.rec_cap, rec_bytes)) != ME_OK) return s;
+    if (r1 <= r0) continue;
+    HIPCHK(c, hipMemcpy2DAsync(d.ref, width, ref + (size_t)y_ref0 * stride, stride, width,
+                               ref_rows, hipMemcpyHostToDevice, d.stream));
+    HIPCHK(c, hipMemcpy2DAsync(d.cur, width, cur + (size_t)y_cur0 * stride, stride, width,
+                               cur_rows, hipMemcpyHostToDevice, d.stream));
+    int16_t* dmv = reinterpret_cast<int16_t*>(d.rec);
+    uint32_t* dcost = reinterpret_cast<uint32_t*>(d.rec + max_blocks * 4);
+    me::SearchArgs p = make_args(d.ref, y_ref0, d.cur, y_cur0, width, height, width, blk, range,
+                                 cost, r0, r1, dmv, dcost);
+    HIPCHK(c, me::launch_search(p, d.stream, nullptr));
+  }
+  Dev& root = c->devs[0];
+  HIPCHK(c, hipSetDevice(root.id));
+  if ((s = grow(c, (void**)&root.gather, &root.gather_cap, rec_bytes * n)) != ME_OK) return s;
+  if (c->distinct) {
+    if ((s = ensure_comms(c)) != ME_OK) return s;
+    NCCLCHK(c, ncclGroupStart());
+    for (int i = 0; i < n; i++) {
+      Dev& d = c->devs[i];
+      NCCLCHK(c, ncclGather(d.rec, i == 0 ? root.gather : nullptr, rec_bytes, ncclUint8, 0,
+                            c->comms[i], d.stream));
+    }
+    NCCLCHK(c, ncclGroupEnd());
+  } else {
+    // Repeated device ids: stripes share a device; device copies stand in for the gather.
+    for (int i = 0; i < n; i++) {
+      Dev& d = c->devs[i];
+      HIPCHK(c, hipStreamSynchronize(d.stream));
+      HIPCHK(c, hipMemcpyPeerAsync(root.gather + i * rec_bytes, root.id, d.rec, d.id, rec_bytes,
+                                   root.stream));
+    }
+  }
+  for (int i = 0; i < n; i++) {
+    HIPCHK(c, hipSetDevice(c->devs[i].id));
+    HIPCHK(c, hipStreamSynchronize(c->devs[i].stream));
+  }
+  HIPCHK(c, hipSetDevice(root.id));
+  std::vector<uint8_t> host(rec_bytes * n);
+  HIPCHK(c, hipMemcpy(host.data(), root.gather, host.size(), hipMemcpyDeviceToHost));
+  for (int i = 0; i < n; i++) {
+    const int nblk = (bounds[i + 1] - bounds[i]) * nbx;
+    const uint8_t* base = host.data() + i * rec_bytes;
+    const size_t off = (size_t)bounds[i] * nbx;
+    memcpy(mv_xy + 2 * off, base, (size_t)nblk * 4);
+    if (block_cost) memcpy(block_cost + off, base + max_blocks * 4, (size_t)nblk * 4);
+  }
+  (void)nby;
+  return ME_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* me_status_str(me_status s) {
+  switch (s) {
+    case ME_OK: return "ok";
+    case ME_EINVAL: return "invalid argument";
+    case ME_ENOMEM: return "out of memory";
+    case ME_EDEVICE: return "device error";
+    case ME_ECOMM: return "communication error";
+    case ME_EUNSUPPORTED: return "unsupported";
+  }
+  return "unknown status";
+}
+
+const char* me_last_error(const me_ctx* ctx) { return ctx ? ctx->err : "null context"; }
+
+const char* me_version(void) { return "me_hip 1 gfx950"; }
+
+int me_num_blocks(int width, int height, int blk) {
+  if (width <= 0 || height <= 0 || blk <= 0) return 0;
+  return ((width + blk - 1) / blk) * ((height + blk - 1) / blk);
+}
+
+uint64_t me_candidate_count(int width, int height, int blk, int range) {
+  if (width <= 0 || height <= 0 || blk <= 0 || range < 0) return 0;
+  uint64_t t = 0;
+  const int nby = (height + blk - 1) / blk;
+  for (int by = 0; by < nby; by++) t += row_candidates(width, height, blk, range, by);
+  return t;
+}
+
+me_status me_plan_stripes(int width, int height, int blk, int range, int n, int* bounds) {
+  if (!bounds || n < 1 || width <= 0 || height <= 0 || blk <= 0 || range < 0) return ME_EINVAL;
+  const int nby = (height + blk - 1) / blk;
+  std::vector<uint64_t> cum(nby + 1, 0);
+  for (int by = 0; by < nby; by++) cum[by + 1] = cum[by] + row_candidates(width, height, blk, range, by);
+  bounds[0] = 0;
+  int r = 0;
+  for (int i = 1; i < n; i++) {
+    const double target = (double)cum[nby] * i / n;
+    while (r < nby && (double)cum[r + 1] <= target) r++;
+    // pick the nearer boundary
+    if (r < nby && target - (double)cum[r] > (double)cum[r + 1] - target) r++;
+    if (r < bounds[i - 1]) r = bounds[i - 1];
+    bounds[i] = r;
+  }
+  bounds[n] = nby;
+  return ME_OK;
+}
+
+me_status me_create(me_ctx** out, const int* device_ids, int n) {
+  if (!out) return ME_EINVAL;
+  *out = nullptr;
+  me_ctx* c = new (std::nothrow) me_ctx();
+  if (!c) return ME_ENOMEM;
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count < 1) {
+    delete c;
+    return ME_EDEVICE;
+  }
+  std::vector<int> ids;
+  if (!device_ids || n <= 0) {
+    int cur = 0;
+    if (hipGetDevice(&cur) != hipSuccess) cur = 0;
+    ids.push_back(cur);
+  } else {
+    for (int i = 0; i < n; i++) {
+      if (device_ids[i] < 0 || device_ids[i] >= count) {
+        delete c;
+        return ME_EINVAL;
+      }
+      ids.push_back(device_ids[i]);
+    }
+  }
+  for (size_t i = 0; i < ids.size(); i++)
+    for (size_t j = 0; j < i; j++)
+      if (ids[i] == ids[j]) c->distinct = false;
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  for (int id : ids) {
+    Dev d;
+    d.id = id;
+    if (hipSetDevice(id) != hipSuccess ||
+        hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking) != hipSuccess) {
+      c->devs.push_back(d);
+      me_destroy(c);
+      (void)hipSetDevice(prev);
+      return ME_EDEVICE;
+    }
+    c->devs.push_back(d);
+  }
+  (void)hipSetDevice(prev);
+  *out = c;
+  return ME_OK;
+}
+
+void me_destroy(me_ctx* c) {
+  if (!c) return;
+  if (c->comms) {
+    for (size_t i = 0; i < c->devs.size(); i++) ncclCommDestroy(c->comms[i]);
+    delete[] c->comms;
+  }
+  for (Dev& d : c->devs) {
+    (void)hipSetDevice(d.id);
+    if (d.stream) (void)hipStreamSynchronize(d.stream);
+    (void)hipFree(d.ref);
+    (void)hipFree(d.rec);
+    (void)hipFree(d.gather);
+    (void)hipFree(d.stats);
+    (void)hipFree(d.out5);
+    if (d.stream) (void)hipStreamDestroy(d.stream);
+  }
+  delete c;
+}
+
+me_status me_full_search(me_ctx* c, const uint8_t* ref, const uint8_t* cur, int width,
+                         int height, int stride, int blk, int range, me_cost cost,
+                         int16_t* mv_xy, uint32_t* block_cost) {
+  me_status s = check_args(c, ref, cur, width, height, stride, blk, range, cost, mv_xy);
+  if (s != ME_OK) return s;
+  c->err[0] = 0;
+  if (c->devs.size() > 1)
+    return multi_search(c, ref, cur, width, height, stride, blk, range, cost, mv_xy, block_cost);
+  Dev& d = c->devs[0];
+  HIPCHK(c, hipSetDevice(d.id));
+  const size_t plane = (size_t)width * height;
+  const size_t nb = (size_t)me_num_blocks(width, height, blk);
+  if ((s = grow(c, (void**)&d.ref, &d.frame_cap, 2 * plane)) != ME_OK) return s;
+  d.cur = d.ref + plane;
+  if ((s = grow(c, (void**)&d.rec, &d.rec_cap, nb * 8)) != ME_OK) return s;
+  HIPCHK(c, hipMemcpy2DAsync(d.ref, width, ref, stride, width, height, hipMemcpyHostToDevice, d.stream));
+  HIPCHK(c, hipMemcpy2DAsync(d.cur, width, cur, stride, width, height, hipMemcpyHostToDevice, d.stream));
+  int16_t* dmv = reinterpret_cast<int16_t*>(d.rec);
+  uint32_t* dcost = reinterpret_cast<uint32_t*>(d.rec + nb * 4);
+  const int nby = (height + blk - 1) / blk;
+  me::SearchArgs p = make_args(d.ref, 0, d.cur, 0, width, height, width, blk, range, cost, 0,
+                               nby, dmv, dcost);
+  HIPCHK(c, me::launch_search(p, d.stream, nullptr));
+  HIPCHK(c, hipMemcpyAsync(mv_xy, dmv, nb * 4, hipMemcpyDeviceToHost, d.stream));
+  if (block_cost)
+    HIPCHK(c, hipMemcpyAsync(block_cost, dcost, nb * 4, hipMemcpyDeviceToHost, d.stream));
+  HIPCHK(c, hipStreamSynchronize(d.stream));
+  return ME_OK;
+}
+
+me_status me_full_search_stripe_device(me_ctx* c, const uint8_t* d_ref, int ref_row0,
+                                       const uint8_t* d_cur, int cur_row0, int width,
+                                       int height, int stride, int blk, int range, me_cost cost,
+                                       int r0, int r1, int16_t* d_mv, uint32_t* d_cost,
+                                       void* stream) {
+  me_status s = check_args(c, d_ref, d_cur, width, height, stride, blk, range, cost, d_mv);
+  if (s != ME_OK) return s;
+  const int nby = (height + blk - 1) / blk;
+  if (r0 < 0 || r1 > nby || r0 > r1) return fail(c, ME_EINVAL, "block rows [%d, %d)", r0, r1);
+  const int need_ref0 = r0 * blk - range > 0 ? r0 * blk - range : 0;
+  if (ref_row0 < 0 || ref_row0 > need_ref0) return fail(c, ME_EINVAL, "ref_row0 %d", ref_row0);
+  if (cur_row0 < 0 || cur_row0 > r0 * blk) return fail(c, ME_EINVAL, "cur_row0 %d", cur_row0);
+  c->err[0] = 0;
+  me::SearchArgs p = make_args(d_ref, ref_row0, d_cur, cur_row0, width, height, stride, blk,
+                               range, cost, r0, r1, d_mv, d_cost);
+  HIPCHK(c, me::launch_search(p, (hipStream_t)stream, nullptr));
+  return ME_OK;
+}
+
+me_status me_full_search_device(me_ctx* c, const uint8_t* d_ref, const uint8_t* d_cur,
+                                int width, int height, int stride, int blk, int range,
+                                me_cost cost, int16_t* d_mv, uint32_t* d_cost, void* stream) {
+  const int nby = blk > 0 ? (height + blk - 1) / blk : 0;
+  return me_full_search_stripe_device(c, d_ref, 0, d_cur, 0, width, height, stride, blk, range,
+                                      cost, 0, nby, d_mv, d_cost, stream);
+}
+
+me_status me_find_best_blocks(me_ctx* c, const int* ref_frame, const int* cur_frame, int width,
+                              int height, int blk, int range, me_ref_block* blks, int num_blks) {
+  me_status s = check_args(c, ref_frame, cur_frame, width, height, width, blk, range,
+                           ME_COST_SSD, blks);
+  if (s != ME_OK) return s;
+  const int nb = me_num_blocks(width, height, blk);
+  if (num_blks != nb) return fail(c, ME_EINVAL, "num_blks %d != %d", num_blks, nb);
+  const size_t plane = (size_t)width * height;
+  std::vector<uint8_t> r8(plane), c8(plane);
+  for (size_t i = 0; i < plane; i++) {  // utils.c:49-53 widened u8 -> int; narrow back
+    r8[i] = (uint8_t)ref_frame[i];
+    c8[i] = (uint8_t)cur_frame[i];
+  }
+  std::vector<int16_t> mv((size_t)nb * 2);
+  s = me_full_search(c, r8.data(), c8.data(), width, height, width, blk, range, ME_COST_SSD,
+                     mv.data(), nullptr);
+  if (s != ME_OK) return s;
+  for (int i = 0; i < nb; i++) {  // populateBlkMotionVector, main.c:11-15
+    blks[i].motion_vectorX = mv[2 * i];
+    blks[i].motion_vectorY = mv[2 * i + 1];
+    blks[i].is_best_match_found = 1;
+  }
+  return ME_OK;
+}
+
+static me_status compensate(me_ctx* c, const uint8_t* ref, const uint8_t* cur, int width,
+                            int height, int blk, const int16_t* mv_xy, uint8_t* out,
+                            int planes, double* psnr) {
+  me_status s = check_args(c, ref, cur ? cur : ref, width, height, width, blk, 0, ME_COST_SSD, mv_xy);
+  if (s != ME_OK) return s;
+  if (!out) return fail(c, ME_EINVAL, "null output");
+  Dev& d = c->devs[0];
+  HIPCHK(c, hipSetDevice(d.id));
+  const size_t plane = (size_t)width * height;
+  const size_t nb = (size_t)me_num_blocks(width, height, blk);
+  if ((s = grow(c, (void**)&d.ref, &d.frame_cap, 2 * plane)) != ME_OK) return s;
+  d.cur = d.ref + plane;
+  if ((s = grow(c, (void**)&d.rec, &d.rec_cap, nb * 8)) != ME_OK) return s;
+  size_t scap = d.stats ? 16 : 0;
+  if ((s = grow(c, (void**)&d.stats, &scap, 16)) != ME_OK) return s;
+  const size_t out_bytes = planes ? 5 * plane : plane;
+  if ((s = grow(c, (void**)&d.out5, &d.out_cap, out_bytes)) != ME_OK) return s;
+  HIPCHK(c, hipMemcpyAsync(d.ref, ref, plane, hipMemcpyHostToDevice, d.stream));
+  HIPCHK(c, hipMemcpyAsync(d.cur, cur ? cur : ref, plane, hipMemcpyHostToDevice, d.stream));
+  HIPCHK(c, hipMemcpyAsync(d.rec, mv_xy, nb * 4, hipMemcpyHostToDevice, d.stream));
+  HIPCHK(c, hipMemsetAsync(d.stats, 0, 16, d.stream));
+  HIPCHK(c, me::launch_compensate(d.ref, d.cur, width, height, blk,
+                                  reinterpret_cast<int16_t*>(d.rec), d.out5, planes, d.stats,
+                                  d.stream));
+  unsigned long long st[2] = {0, 0};
+  HIPCHK(c, hipMemcpyAsync(out, d.out5, out_bytes, hipMemcpyDeviceToHost, d.stream));
+  HIPCHK(c, hipMemcpyAsync(st, d.stats, 16, hipMemcpyDeviceToHost, d.stream));
+  HIPCHK(c, hipStreamSynchronize(d.stream));
+  if (psnr) {  // utils.c:147-154, double arithmetic on the exact integer sum
+    double mse = (double)st[0];
+    mse /= (double)width * height;
+    *psnr = mse == 0 ? 99.0 : 20 * log10((double)st[1]) - 10 * log10(mse);
+  }
+  return ME_OK;
+}
+
+me_status me_motion_compensate(me_ctx* c, const uint8_t* ref, int width, int height, int blk,
+                               const int16_t* mv_xy, uint8_t* mc) {
+  return compensate(c, ref, nullptr, width, height, blk, mv_xy, mc, 0, nullptr);
+}
+
+me_status me_compensate_planes(me_ctx* c, const uint8_t* ref, const uint8_t* cur, int width,
+                               int height, int blk, const int16_t* mv_xy, uint8_t* out5,
+                               double* psnr) {
+  if (!cur) return fail(c, ME_EINVAL, "null cur");
+  return compensate(c, ref, cur, width, height, blk, mv_xy, out5, 1, psnr);
+}
+
+}  // extern "C"

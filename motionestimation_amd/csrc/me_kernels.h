@@ -1,0 +1,53 @@
+// me_kernels.h -- device-side launch interface (internal to libme_hip.so).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace me {
+
+enum { COST_SSD = 0, COST_SAD = 1 };
+
+constexpr int GENERIC_THREADS = 256;
+constexpr int GENERIC_LDS_BUDGET = 60 * 1024;
+constexpr int QSAD_LDS_BUDGET = 96 * 1024;
+
+// One search launch: block rows [block_row_begin, block_row_end) of a
+// width x height frame.  ref / cur point at frame rows ref_row0 / cur_row0.
+// Outputs are indexed (block row - block_row_begin) * nbx + block column.
+struct SearchArgs {
+  const uint8_t* ref;
+  const uint8_t* cur;
+  int ref_row0, cur_row0;
+  int width, height, stride;
+  int blk, range;
+  int nbx;
+  int block_row_begin, block_row_end;
+  int cost_kind;
+  int16_t* mv;
+  uint32_t* cost;
+};
+
+struct QsadGeom {
+  int tb;          // blocks per workgroup
+  int groups;      // 4-wide dx groups per block
+  int chunks;      // K-row dy chunks
+  int pitch;       // LDS tile row pitch (bytes)
+  int threads;     // workgroup size
+  int lds;         // dynamic LDS bytes
+  int wg_per_row;  // workgroups per block row
+  int nbx_full;    // full-width blocks per row
+  int aligned;     // 4-byte aligned global rows
+};
+
+hipError_t launch_search(const SearchArgs& p, hipStream_t stream, int* used_fast);
+hipError_t launch_generic(const SearchArgs& p, int bx0, int nbx_range, int nrows,
+                          hipStream_t stream);
+bool plan_qsad(const SearchArgs& p, QsadGeom* g, int* k_out);
+
+// Consumers of the MV field (me_post.hip).
+hipError_t launch_compensate(const uint8_t* ref, const uint8_t* cur, int width, int height,
+                             int blk, const int16_t* mv, uint8_t* out5, int write_planes,
+                             unsigned long long* stats, hipStream_t stream);
+
+}  // namespace me

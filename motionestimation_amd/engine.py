@@ -1,0 +1,148 @@
+"""Host-side engine over libme_hip.so.
+
+``Engine.full_search`` is the frame-level drop-in for the reference's dispatch
+region (src/cpu/main.c:144-158): one call searches every block of the frame on
+the GPU and returns the MV field plus per-block cost.  ``full_search_device``
+works on HBM-resident torch tensors and enqueues on a stream (what bench.py
+times); ``search_stripe_device`` is the per-rank unit of the row-stripe shard.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import ME_COST_SAD, ME_COST_SSD, MEError, check
+
+_COST = {"ssd": ME_COST_SSD, "mse": ME_COST_SSD, "sad": ME_COST_SAD,
+         ME_COST_SSD: ME_COST_SSD, ME_COST_SAD: ME_COST_SAD}
+
+
+def cost_code(cost) -> int:
+    try:
+        return _COST[cost]
+    except KeyError:
+        raise MEError(_lib.ME_EINVAL, f"unknown cost {cost!r}") from None
+
+
+def num_blocks(width: int, height: int, blk: int) -> int:
+    return int(_lib.lib().me_num_blocks(width, height, blk))
+
+
+def candidate_count(width: int, height: int, blk: int, span: int) -> int:
+    return int(_lib.lib().me_candidate_count(width, height, blk, span))
+
+
+def plan_stripes(width: int, height: int, blk: int, span: int, shards: int) -> list:
+    """Block-row boundaries [b0=0, ..., b_n=nby] balancing exact candidate counts."""
+    out = (ctypes.c_int * (shards + 1))()
+    check(_lib.lib().me_plan_stripes(width, height, blk, span, shards, out))
+    return list(out)
+
+
+def version() -> str:
+    return _lib.lib().me_version().decode()
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+class Engine:
+    """One context: device buffers, a HIP stream per device, RCCL comms when
+    created over several distinct devices.  Use from one thread at a time."""
+
+    def __init__(self, devices=None):
+        L = _lib.lib()
+        h = ctypes.c_void_p()
+        if devices:
+            ids = (ctypes.c_int * len(devices))(*devices)
+            st = L.me_create(ctypes.byref(h), ids, len(devices))
+        else:
+            st = L.me_create(ctypes.byref(h), None, 0)
+        check(st)
+        self._h = h
+        self.devices = list(devices) if devices else None
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            _lib.lib().me_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # ------------------------------------------------------------- host API
+    def full_search(self, ref, cur, blk: int, span: int, cost="ssd", stride=None):
+        """Search (H, W) uint8 planes.  Returns (mv int16 [nblocks, 2] as
+        (mvx, mvy), cost uint32 [nblocks]) in the reference's raster order."""
+        ref = np.ascontiguousarray(ref, dtype=np.uint8)
+        cur = np.ascontiguousarray(cur, dtype=np.uint8)
+        if ref.ndim != 2 or ref.shape != cur.shape:
+            raise MEError(_lib.ME_EINVAL, f"plane shapes {ref.shape} vs {cur.shape}")
+        h, w = ref.shape
+        n = num_blocks(w, h, blk) if blk > 0 else 0
+        mv = np.zeros((max(n, 1), 2), np.int16)
+        cst = np.zeros(max(n, 1), np.uint32)
+        check(_lib.lib().me_full_search(self._h, _ptr(ref), _ptr(cur), w, h, stride or w, blk,
+                                        span, cost_code(cost), _ptr(mv), _ptr(cst)), self._h)
+        return mv[:n], cst[:n]
+
+    def compensate_planes(self, ref, cur, blk: int, mv):
+        """5-plane output [ref, cur, mc, |ref-cur|, |mc-cur|] (5H, W) and PSNR."""
+        ref = np.ascontiguousarray(ref, np.uint8)
+        cur = np.ascontiguousarray(cur, np.uint8)
+        mv = np.ascontiguousarray(mv, np.int16)
+        h, w = ref.shape
+        out = np.zeros((5 * h, w), np.uint8)
+        psnr = ctypes.c_double()
+        check(_lib.lib().me_compensate_planes(self._h, _ptr(ref), _ptr(cur), w, h, blk,
+                                              _ptr(mv), _ptr(out), ctypes.byref(psnr)), self._h)
+        return out, psnr.value
+
+    def motion_compensate(self, ref, blk: int, mv):
+        ref = np.ascontiguousarray(ref, np.uint8)
+        mv = np.ascontiguousarray(mv, np.int16)
+        h, w = ref.shape
+        mc = np.zeros_like(ref)
+        check(_lib.lib().me_motion_compensate(self._h, _ptr(ref), w, h, blk, _ptr(mv),
+                                              _ptr(mc)), self._h)
+        return mc
+
+    # ----------------------------------------------------------- device API
+    def full_search_device(self, ref_t, cur_t, blk: int, span: int, cost, mv_t, cost_t=None,
+                           stream=None, width=None, height=None, stride=None):
+        """Enqueue a search on HBM-resident uint8 torch tensors (H, W); mv_t is an
+        int16 tensor [nblocks, 2], cost_t uint32/int32 [nblocks] or None."""
+        h, w = (height, width) if height else tuple(ref_t.shape[-2:])
+        st = stream if stream is not None else _current_stream()
+        check(_lib.lib().me_full_search_device(
+            self._h, ref_t.data_ptr(), cur_t.data_ptr(), w, h, stride or w, blk, span,
+            cost_code(cost), mv_t.data_ptr(), cost_t.data_ptr() if cost_t is not None else None,
+            st), self._h)
+
+    def search_stripe_device(self, ref_t, ref_row0: int, cur_t, cur_row0: int, width: int,
+                             height: int, blk: int, span: int, cost, row_begin: int,
+                             row_end: int, mv_t, cost_t=None, stream=None, stride=None):
+        """One row stripe (block rows [row_begin, row_end)) on resident planes that
+        start at frame rows ref_row0 / cur_row0."""
+        st = stream if stream is not None else _current_stream()
+        check(_lib.lib().me_full_search_stripe_device(
+            self._h, ref_t.data_ptr(), ref_row0, cur_t.data_ptr(), cur_row0, width, height,
+            stride or width, blk, span, cost_code(cost), row_begin, row_end, mv_t.data_ptr(),
+            cost_t.data_ptr() if cost_t is not None else None, st), self._h)
+
+
+def _current_stream():
+    import torch
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)

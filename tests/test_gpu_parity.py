@@ -1,0 +1,253 @@
+"""GPU parity: the HIP path through the C ABI against the reference goldens
+and the oracle, bit-exact (integer MVs and costs; the reference's float MSE
+score reproduced bit for bit)."""
+import os
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+import motionestimation_amd as me
+from motionestimation_amd import synth
+
+pytestmark = pytest.mark.gpu
+NT = min(16, os.cpu_count() or 1)
+
+
+def _mse_bits(cost, blk, w, h):
+    """(float)SSD / (float)(bw*bh) per block, as the reference rounds it."""
+    nbx, nby = (w + blk - 1) // blk, (h + blk - 1) // blk
+    bw = np.minimum(blk, w - np.arange(nbx) * blk)
+    bh = np.minimum(blk, h - np.arange(nby) * blk)
+    area = (bh[:, None] * bw[None, :]).reshape(-1).astype(np.float32)
+    return (cost.astype(np.float32) / area).view(np.uint32)
+
+
+def test_golden_cases_ssd(engine, manifest):
+    """Every golden case from the unmodified reference: same MVs; MSE bits."""
+    for c in manifest["cases"]:
+        if c["width"] > 2000:
+            continue
+        cur, ref = O.load_frame(c["cur"], manifest), O.load_frame(c["ref"], manifest)
+        gmv, gmse = O.load_case(c)
+        mv, cost = engine.full_search(ref, cur, c["blk"], c["span"], "ssd")
+        np.testing.assert_array_equal(mv.astype(np.int32), gmv, err_msg=c["name"])
+        if c["blk"] <= 16:
+            np.testing.assert_array_equal(_mse_bits(cost, c["blk"], c["width"], c["height"]),
+                                          gmse.view(np.uint32), err_msg=c["name"])
+        # cost = integer SSD of the reference's chosen vector
+        _, ossd, _ = O.full_search(ref, cur, c["blk"], c["span"], "mse", threads=NT)
+        np.testing.assert_array_equal(cost, ossd, err_msg=c["name"])
+
+
+def test_golden_cases_sad(engine, manifest):
+    for c in manifest["cases"]:
+        if c["width"] > 2000:
+            continue
+        cur, ref = O.load_frame(c["cur"], manifest), O.load_frame(c["ref"], manifest)
+        mv, cost = engine.full_search(ref, cur, c["blk"], c["span"], "sad")
+        omv, ocost, _ = O.full_search(ref, cur, c["blk"], c["span"], "sad", threads=NT)
+        np.testing.assert_array_equal(mv, omv, err_msg=c["name"])
+        np.testing.assert_array_equal(cost, ocost, err_msg=c["name"])
+
+
+@pytest.mark.parametrize("blk", [8, 16])
+@pytest.mark.parametrize("span", [0, 1, 2, 3, 5, 7, 16, 32, 33])
+def test_fast_sad_kernel_shapes(engine, blk, span):
+    """qsad kernel across dx alignments (S mod 4), chunk padding, partial
+    bottom rows (H % B != 0) and a partial right column (W % B != 0)."""
+    rng = np.random.default_rng(blk * 100 + span)
+    for (h, w) in [(72, 96), (75, 100), (40, 200)]:
+        ref = synth._box5(rng.integers(0, 256, (h, w), dtype=np.uint8))
+        cur = np.clip(synth.shift_plane(ref, 2, -1).astype(int) + rng.integers(-3, 4, (h, w)), 0,
+                      255).astype(np.uint8)
+        mv, cost = engine.full_search(ref, cur, blk, span, "sad")
+        omv, ocost, _ = O.full_search(ref, cur, blk, span, "sad", threads=NT)
+        np.testing.assert_array_equal(mv, omv, err_msg=f"{h}x{w} B{blk} S{span}")
+        np.testing.assert_array_equal(cost, ocost)
+
+
+def test_ties_flat_frame_sad(engine):
+    """Flat frames: all candidates tie; the raster-first one must win."""
+    ref = np.full((64, 96), 77, np.uint8)
+    for blk, span in [(16, 32), (8, 13), (16, 7)]:
+        mv, cost = engine.full_search(ref, ref, blk, span, "sad")
+        omv, ocost, _ = O.full_search(ref, ref, blk, span, "sad")
+        np.testing.assert_array_equal(mv, omv)
+        assert (cost == 0).all()
+
+
+def test_stride_and_device_api(engine):
+    import torch
+    rng = np.random.default_rng(3)
+    h, w, blk, span = 96, 130, 16, 9
+    big_ref = rng.integers(0, 256, (h, w + 6), dtype=np.uint8)
+    big_cur = rng.integers(0, 256, (h, w + 6), dtype=np.uint8)
+    ref, cur = big_ref[:, :w].copy(), big_cur[:, :w].copy()
+    omv, ocost, _ = O.full_search(ref, cur, blk, span, "sad")
+    # host API with a padded pitch
+    mv, cost = engine.full_search(big_ref, big_cur, blk, span, "sad")  # full width first
+    n = me.num_blocks(w, h, blk)
+    L = me._lib.lib()
+    mv2 = np.zeros((n, 2), np.int16)
+    c2 = np.zeros(n, np.uint32)
+    me._lib.check(L.me_full_search(engine._h, big_ref.ctypes.data, big_cur.ctypes.data, w, h,
+                                   w + 6, blk, span, 1, mv2.ctypes.data, c2.ctypes.data),
+                  engine._h)
+    np.testing.assert_array_equal(mv2, omv)
+    np.testing.assert_array_equal(c2, ocost)
+    # device API on HBM-resident tensors
+    rt = torch.from_numpy(ref).cuda()
+    ct = torch.from_numpy(cur).cuda()
+    mvt = torch.zeros((n, 2), dtype=torch.int16, device="cuda")
+    cot = torch.zeros(n, dtype=torch.int32, device="cuda")
+    engine.full_search_device(rt, ct, blk, span, "sad", mvt, cot)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(mvt.cpu().numpy(), omv)
+    np.testing.assert_array_equal(cot.cpu().numpy().view(np.uint32), ocost)
+
+
+def test_stripe_device_api_halo_only(engine):
+    """Each stripe sees only its cur rows + S-row ref halo (device pointers
+    offset to the stripe origin); concatenated stripes == full frame."""
+    import torch
+    from motionestimation_amd import shard
+    ref, cur = synth.frame_pair(640, 360, 11, 4, -2)
+    for blk, span, cost, world in [(16, 32, "sad", 3), (8, 12, "ssd", 4), (16, 7, "sad", 5)]:
+        omv, ocost, _ = O.full_search(ref, cur, blk, span, cost, threads=NT)
+        mvs, costs = [], []
+        for st in shard.plan(640, 360, blk, span, world):
+            rt = torch.from_numpy(ref[st.ref_y0:st.ref_y1].copy()).cuda()
+            ct = torch.from_numpy(cur[st.cur_y0:st.cur_y1].copy()).cuda()
+            n = max(st.nblocks, 1)
+            mvt = torch.zeros((n, 2), dtype=torch.int16, device="cuda")
+            cot = torch.zeros(n, dtype=torch.int32, device="cuda")
+            if st.nblocks:
+                engine.search_stripe_device(rt, st.ref_y0, ct, st.cur_y0, 640, 360, blk, span, cost,
+                                            st.row_begin, st.row_end, mvt, cot)
+            torch.cuda.synchronize()
+            mvs.append(mvt.cpu().numpy()[:st.nblocks])
+            costs.append(cot.cpu().numpy().view(np.uint32)[:st.nblocks])
+        np.testing.assert_array_equal(np.concatenate(mvs), omv)
+        np.testing.assert_array_equal(np.concatenate(costs), ocost)
+
+
+def test_multi_shard_context_on_one_gpu():
+    """A context over device ids [0, 0, 0]: stripes + gather inside the library."""
+    ref, cur = synth.frame_pair(320, 240, 5, -3, 2)
+    with me.Engine(devices=[0, 0, 0]) as eng:
+        for cost in ("sad", "ssd"):
+            mv, c = eng.full_search(ref, cur, 16, 16, cost)
+            omv, oc, _ = O.full_search(ref, cur, 16, 16, cost)
+            np.testing.assert_array_equal(mv, omv)
+            np.testing.assert_array_equal(c, oc)
+
+
+def test_reference_adapter_and_interface(engine, manifest):
+    """create_prediction_frame / find_best_blks / output planes as the reference
+    driver uses them; the published output_4_{7,15}.yuv and PSNR reproduce."""
+    f1, f4 = O.load_frame("ForemanYF1", manifest), O.load_frame("ForemanYF4", manifest)
+    for key, info in manifest["published"].items():
+        pf = me.create_prediction_frame(f4, 352, 288, info["blk"])
+        me.find_best_blks(pf, f1, info["span"], engine=engine)
+        planes, psnr = me.output_planes(pf, f1, engine=engine)
+        pub = np.fromfile(os.path.join(O.GOLDEN, info["file"]), np.uint8).reshape(5 * 288, 352)
+        np.testing.assert_array_equal(planes, pub, err_msg=key)
+    pf = me.create_prediction_frame(f4, 352, 288, 8)
+    scores = me.find_best_blks(pf, f1, 12, engine=engine)
+    _, psnr = me.output_planes(pf, f1, engine=engine)
+    assert "%.6f" % psnr == "31.816000"
+    g = [c for c in manifest["cases"] if c["name"] == "foreman41_b8_s12"][0]
+    _, gmse = O.load_case(g)
+    np.testing.assert_array_equal(scores.view(np.uint32), gmse.view(np.uint32))
+
+
+def test_c_adapter_fills_reference_block_records(engine, manifest):
+    import ctypes
+    f1, f2 = O.load_frame("ForemanYF1", manifest), O.load_frame("ForemanYF2", manifest)
+    n = me.num_blocks(352, 288, 16)
+
+    class Blk(ctypes.Structure):
+        _fields_ = [(f, ctypes.c_int) for f in (
+            "idx_x", "idx_y", "top_left_x", "top_left_y", "bottom_right_x", "bottom_right_y",
+            "width", "height", "is_best_match_found", "motion_vectorX", "motion_vectorY")]
+
+    assert ctypes.sizeof(Blk) == 44
+    blks = (Blk * n)()
+    r32, c32 = f1.astype(np.int32), f2.astype(np.int32)
+    me._lib.check(me._lib.lib().me_find_best_blocks(engine._h, r32.ctypes.data, c32.ctypes.data,
+                                                     352, 288, 16, 16, blks, n), engine._h)
+    g = [c for c in manifest["cases"] if c["name"] == "foreman21_b16_s16"][0]
+    gmv, _ = O.load_case(g)
+    got = np.array([[b.motion_vectorX, b.motion_vectorY] for b in blks])
+    np.testing.assert_array_equal(got, gmv)
+    assert all(b.is_best_match_found == 1 for b in blks)
+
+
+def test_error_paths(engine):
+    ref = np.zeros((32, 32), np.uint8)
+    for blk, span in [(0, 4), (65, 4), (8, -1), (8, 5000)]:
+        with pytest.raises(me.MEError) as ei:
+            engine.full_search(ref, ref, blk, span, "sad")
+        assert ei.value.status == me._lib.ME_EINVAL
+    with pytest.raises(me.MEError):
+        engine.full_search(ref, ref, 8, 4, "nope")
+
+
+@pytest.mark.slow
+def test_full_1080p_both_costs(engine, manifest):
+    """BASELINE configs[2] at full size: SSD vs the reference golden, SAD vs oracle."""
+    c = [c for c in manifest["cases"] if c["name"] == "synth1080p_b16_s32"][0]
+    ref, cur = synth.named_pair("1080p")
+    gmv, gmse = O.load_case(c)
+    mv, cost = engine.full_search(ref, cur, 16, 32, "ssd")
+    np.testing.assert_array_equal(mv.astype(np.int32), gmv)
+    np.testing.assert_array_equal(_mse_bits(cost, 16, 1920, 1080), gmse.view(np.uint32))
+    mv, cost = engine.full_search(ref, cur, 16, 32, "sad")
+    omv, ocost, _ = O.full_search(ref, cur, 16, 32, "sad", threads=NT)
+    np.testing.assert_array_equal(mv, omv)
+    np.testing.assert_array_equal(cost, ocost)
+
+
+@pytest.mark.slow
+def test_full_4k_ssd_golden_and_sad_properties(engine, manifest):
+    """BASELINE configs[3]: SSD vs the reference golden (full frame); SAD vs the
+    oracle on sampled block rows (top, middle, bottom)."""
+    c = [c for c in manifest["cases"] if c["name"] == "synth4k_b16_s64"][0]
+    ref, cur = synth.named_pair("4k")
+    gmv, gmse = O.load_case(c)
+    mv, cost = engine.full_search(ref, cur, 16, 64, "ssd")
+    np.testing.assert_array_equal(mv.astype(np.int32), gmv)
+    np.testing.assert_array_equal(_mse_bits(cost, 16, 3840, 2160), gmse.view(np.uint32))
+    mv, cost = engine.full_search(ref, cur, 16, 64, "sad")
+    nbx = 240
+    for row in (0, 67, 134):
+        omv, ocost, _ = O.full_search(ref, cur, 16, 64, "sad", threads=NT, begin=row * nbx,
+                                      end=(row + 1) * nbx)
+        np.testing.assert_array_equal(mv[row * nbx:(row + 1) * nbx], omv)
+        np.testing.assert_array_equal(cost[row * nbx:(row + 1) * nbx], ocost)
+
+
+@pytest.mark.slow
+def test_8k_b8_s128_sampled(engine):
+    """BASELINE configs[4] (8x8, +-128, 7680x4320): full GPU frame, oracle on
+    sampled block rows; SAD lower-bounded by the zero-vector... property:
+    cost <= SAD at the true shift for interior blocks."""
+    ref, cur = synth.named_pair("8k")
+    mv, cost = engine.full_search(ref, cur, 8, 128, "sad")
+    nbx = 960
+    for row in (0, 270, 539):
+        omv, ocost, _ = O.full_search(ref, cur, 8, 128, "sad", threads=NT, begin=row * nbx,
+                                      end=row * nbx + 96)
+        np.testing.assert_array_equal(mv[row * nbx:row * nbx + 96], omv)
+        np.testing.assert_array_equal(cost[row * nbx:row * nbx + 96], ocost)
+    # property over the whole frame: the chosen cost never exceeds the SAD of
+    # the generator's true displacement (cur = ref shifted by (+40, -27)).
+    r = ref.astype(np.int32)
+    c = cur.astype(np.int32)
+    nby = 540
+    for by in range(2, nby - 6, 97):
+        for bx in range(6, nbx - 6, 131):
+            y, x = by * 8, bx * 8
+            true_sad = np.abs(c[y:y + 8, x:x + 8] - r[y + 27:y + 35, x - 40:x - 32]).sum()
+            assert cost[by * nbx + bx] <= true_sad

@@ -1,0 +1,120 @@
+"""The oracle (CPU restatement) pinned against the REAL reference.
+
+Golden MV/MSE records come from oracle/_ref/ref_dump (unmodified reference
+objects, see tests/golden/make_golden.py); the MC planes from the reference's
+published results/cpu/foreman/output_4_{7,15}.yuv.
+"""
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+
+
+def _cases(manifest, big=False):
+    return [c for c in manifest["cases"] if c["cur"].startswith("synth:") == big]
+
+
+def test_golden_files_intact(manifest):
+    for c in manifest["cases"]:
+        raw = open(os.path.join(O.GOLDEN, c["mv"]), "rb").read()
+        assert hashlib.sha256(raw).hexdigest() == c["sha256"], c["name"]
+    for key, info in manifest["frames"].items():
+        if "file" in info:
+            raw = open(os.path.join(O.GOLDEN, info["file"]), "rb").read()
+            assert hashlib.sha256(raw).hexdigest() == info["sha256"], key
+
+
+def test_oracle_mse_bitexact_vs_reference(manifest):
+    """Float-MSE restatement == reference: MVs and the float score bit for bit."""
+    for c in _cases(manifest):
+        cur, ref = O.load_frame(c["cur"], manifest), O.load_frame(c["ref"], manifest)
+        gmv, gmse = O.load_case(c)
+        mv, _, mse = O.full_search(ref, cur, c["blk"], c["span"], "mse")
+        np.testing.assert_array_equal(mv.astype(np.int32), gmv, err_msg=c["name"])
+        np.testing.assert_array_equal(mse.view(np.uint32), gmse.view(np.uint32), err_msg=c["name"])
+
+
+def test_integer_ssd_argmin_equals_float_mse(manifest):
+    """integer SSD with raster-first ties picks the reference's
+    vector; for w*h <= 256, (float)SSD/(w*h) is the reference's score exactly."""
+    for c in _cases(manifest):
+        cur, ref = O.load_frame(c["cur"], manifest), O.load_frame(c["ref"], manifest)
+        gmv, gmse = O.load_case(c)
+        mv, ssd, mse = O.full_search(ref, cur, c["blk"], c["span"], "ssd")
+        np.testing.assert_array_equal(mv.astype(np.int32), gmv, err_msg=c["name"])
+        if c["blk"] <= 16:
+            np.testing.assert_array_equal(mse.view(np.uint32), gmse.view(np.uint32),
+                                          err_msg=c["name"])
+
+
+@pytest.mark.slow
+def test_oracle_full_size_golden(manifest):
+    for c in _cases(manifest, big=True):
+        if c["width"] > 2000:
+            continue  # 4K is covered on the GPU box
+        cur, ref = O.load_frame(c["cur"], manifest), O.load_frame(c["ref"], manifest)
+        gmv, gmse = O.load_case(c)
+        mv, ssd, mse = O.full_search(ref, cur, c["blk"], c["span"], "ssd")
+        np.testing.assert_array_equal(mv.astype(np.int32), gmv, err_msg=c["name"])
+        np.testing.assert_array_equal(mse.view(np.uint32), gmse.view(np.uint32))
+
+
+def test_published_mc_planes(manifest):
+    """output_4_{7,15}.yuv published by the reference == oracle's 5 planes."""
+    ref = O.load_frame("ForemanYF1", manifest)
+    cur = O.load_frame("ForemanYF4", manifest)
+    for key, info in manifest["published"].items():
+        pub = np.fromfile(os.path.join(O.GOLDEN, info["file"]), np.uint8).reshape(5, 288, 352)
+        mv, _, _ = O.full_search(ref, cur, info["blk"], info["span"], "mse")
+        mc = O.motion_compensate(ref, info["blk"], mv)
+        np.testing.assert_array_equal(pub[0], ref)
+        np.testing.assert_array_equal(pub[1], cur)
+        np.testing.assert_array_equal(pub[2], mc, err_msg=key)
+        np.testing.assert_array_equal(pub[3], np.abs(ref.astype(int) - cur).astype(np.uint8))
+        np.testing.assert_array_equal(pub[4], np.abs(mc.astype(int) - cur).astype(np.uint8))
+
+
+def test_published_psnr(manifest):
+    """results/cpu/foreman/2990wx_threadripper_64_cores.txt:10 and 8_12.txt:10."""
+    f1, f4 = O.load_frame("ForemanYF1", manifest), O.load_frame("ForemanYF4", manifest)
+    mv, _, _ = O.full_search(f1, f4, 8, 12, "mse")
+    assert "%.6f" % O.psnr(O.motion_compensate(f1, 8, mv), f4) == "31.816000"
+    mv, _, _ = O.full_search(f4, f1, 8, 12, "mse")
+    assert "%.6f" % O.psnr(O.motion_compensate(f4, 8, mv), f1) == "31.750712"
+
+
+def test_candidate_counts():
+    """Exact counts quoted in BASELINE.md / SURVEY §8d."""
+    assert O.candidate_count(352, 288, 8, 12) == 927_024
+    assert O.candidate_count(3840, 2160, 8, 12) == 80_401_024
+    assert O.candidate_count(352, 288, 16, 7) == 80_896
+    assert O.candidate_count(352, 288, 16, 16) == 390_028
+    assert O.candidate_count(1920, 1080, 16, 32) == 33_188_832
+    assert O.candidate_count(3840, 2160, 16, 64) == 523_790_800
+    assert O.candidate_count(7680, 4320, 8, 128) == 33_405_688_576
+
+
+def test_sad_restatement_small_bruteforce():
+    """The SAD variant (no reference counterpart) against a numpy brute force
+    with the same loops: candidates y outer, x inner, strict < ."""
+    rng = np.random.default_rng(7)
+    for (h, w, blk, span) in [(20, 27, 6, 4), (16, 16, 16, 3), (13, 9, 4, 5)]:
+        ref = rng.integers(0, 256, (h, w), dtype=np.uint8)
+        cur = rng.integers(0, 256, (h, w), dtype=np.uint8)
+        mv, cost, _ = O.full_search(ref, cur, blk, span, "sad")
+        nbx = (w + blk - 1) // blk
+        for i in range(len(mv)):
+            bx, by = i % nbx, i // nbx
+            tlx, tly = bx * blk, by * blk
+            bw, bh = min(blk, w - tlx), min(blk, h - tly)
+            c = cur[tly:tly + bh, tlx:tlx + bw].astype(int)
+            best = None
+            for y in range(max(tly - span, 0), min(tly + bh - 1 + span, h - 1) - bh + 2):
+                for x in range(max(tlx - span, 0), min(tlx + bw - 1 + span, w - 1) - bw + 2):
+                    s = int(np.abs(c - ref[y:y + bh, x:x + bw]).sum())
+                    if best is None or s < best[0]:
+                        best = (s, x - tlx, y - tly)
+            assert (cost[i], mv[i, 0], mv[i, 1]) == best
