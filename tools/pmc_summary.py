@@ -1,0 +1,91 @@
+#!/usr/bin/env python3
+"""Fold rocprofv3 outputs of tools/profile.sh into profiles/.
+
+HBM bytes per launch follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE
+are in KiB (x1024); on gfx950 FETCH_SIZE reports exactly half the bytes of a
+wide coalesced (16 B/lane) streaming read, so it is doubled; WRITE_SIZE is
+exact for such stores.  The counters come from separate passes.
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+out_dir, tag = sys.argv[1], sys.argv[2]
+args = sys.argv[3:]
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PROF = os.path.join(REPO, "profiles")
+os.makedirs(PROF, exist_ok=True)
+
+
+def rows(pattern):
+    files = glob.glob(os.path.join(out_dir, "**", pattern), recursive=True)
+    out = []
+    for f in files:
+        with open(f) as fh:
+            out.extend(csv.DictReader(fh))
+    return out, files
+
+
+stats, sfiles = rows("*kernel_stats.csv")
+for f in sfiles:
+    shutil.copy(f, os.path.join(PROF, f"{tag}_kernel_stats.csv"))
+ktrace, _ = rows("*kernel_trace.csv")
+
+
+def is_me(name):
+    return "me_" in name or "qsad" in name or "generic" in name
+
+
+def counter(pattern, cname):
+    rs, _ = rows(pattern)
+    per = {}
+    for r in rs:
+        name = r.get("Kernel_Name") or r.get("Kernel-Name") or ""
+        if r.get("Counter_Name") != cname or not is_me(name):
+            continue
+        per.setdefault(name, []).append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in per.items()}
+
+
+fetch = counter("*counter_collection.csv", "FETCH_SIZE")
+write = counter("*counter_collection.csv", "WRITE_SIZE")
+summary = {}
+for r in stats:
+    name = r.get("Name", "")
+    if not is_me(name):
+        continue
+    summary[name] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
+                     "min_ns": float(r["MinNs"]), "max_ns": float(r["MaxNs"])}
+for name, v in fetch.items():
+    summary.setdefault(name, {})["fetch_kib"] = v
+for name, v in write.items():
+    summary.setdefault(name, {})["write_kib"] = v
+dom = max(summary, key=lambda k: summary[k].get("avg_ns", 0) * summary[k].get("calls", 0))
+d = summary[dom]
+hbm = None
+if "fetch_kib" in d and "write_kib" in d:
+    hbm = 2 * d["fetch_kib"] * 1024 + d["write_kib"] * 1024
+bench_tag = None
+cfg = "1080p"
+cost = "sad"
+for i, a in enumerate(args):
+    if a == "--config":
+        cfg = args[i + 1]
+    if a == "--cost":
+        cost = args[i + 1]
+blk, span = {"1080p": (16, 32), "4k": (16, 64), "8k": (8, 128)}[cfg]
+bench_tag = f"{cfg}_b{blk}_s{span}_{cost}"
+path = os.path.join(PROF, "pmc_summary.json")
+try:
+    allsum = json.load(open(path))
+except (OSError, ValueError):
+    allsum = {}
+allsum[bench_tag] = {"profile_tag": tag, "dominant_kernel": dom, "kernels": summary,
+                     "hbm_bytes_per_launch": hbm,
+                     "note": "hbm = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 correction, "
+                             "MI355X_MICROARCH.md §HBM); separate --pmc passes"}
+json.dump(allsum, open(path, "w"), indent=1)
+print(json.dumps(allsum[bench_tag], indent=1))

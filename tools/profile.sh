@@ -1,0 +1,20 @@
+#!/bin/bash
+# Profile the bench workload on the GPU box (run from the repo root):
+#   tools/profile.sh <tag> [bench args...]
+# 1) rocprofv3 --kernel-trace --stats  (per-kernel durations)
+# 2) rocprofv3 --pmc FETCH_SIZE        (own pass: TCC slots, MI355X_MICROARCH.md)
+# 3) rocprofv3 --pmc WRITE_SIZE        (own pass)
+# then tools/pmc_summary.py folds them into profiles/pmc_summary.json and
+# copies the stats CSVs to profiles/<tag>_*.
+set -o pipefail
+TAG=${1:-r01}
+shift
+ARGS=${@:---steps 20 --warmup 3 --no-cpu}
+OUT=gpurun_out/prof_$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -d "$OUT/kt" -o run --output-format csv -- python3 bench.py $ARGS > "$OUT/kt.log" 2>&1 || exit $?
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -T -d "$OUT/fetch" -o run --output-format csv -- python3 bench.py $ARGS > "$OUT/fetch.log" 2>&1 || exit $?
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -T -d "$OUT/write" -o run --output-format csv -- python3 bench.py $ARGS > "$OUT/write.log" 2>&1 || exit $?
+find "$OUT" -name "*.csv" | head -50
+python3 tools/pmc_summary.py "$OUT" "$TAG" $ARGS
