@@ -116,6 +116,13 @@ me::SearchArgs make_args(const uint8_t* ref, int ref_row0, const uint8_t* cur, i
   p.cost_kind = cost;
   p.mv = mv;
   p.cost = cst;
+  // Bytes the kernels may read from each plane (the DMA descriptors' range):
+  // the rows the stripe contract guarantees resident (include/me.h).
+  const int ref_end = r1 * blk + range < height ? r1 * blk + range : height;
+  const int cur_end = r1 * blk < height ? r1 * blk : height;
+  const long ref_rows = ref_end - ref_row0, cur_rows = cur_end - cur_row0;
+  p.ref_bytes = ref_rows > 0 ? (uint32_t)((ref_rows - 1) * (long)stride + width) : 0;
+  p.cur_bytes = cur_rows > 0 ? (uint32_t)((cur_rows - 1) * (long)stride + width) : 0;
   return p;
 }
 

@@ -10,7 +10,7 @@ enum { COST_SSD = 0, COST_SAD = 1 };
 
 constexpr int GENERIC_THREADS = 256;
 constexpr int GENERIC_LDS_BUDGET = 60 * 1024;
-constexpr int QSAD_LDS_BUDGET = 96 * 1024;
+constexpr int QSAD_LDS_BUDGET = 80 * 1024;
 
 // One search launch: block rows [block_row_begin, block_row_end) of a
 // width x height frame.  ref / cur point at frame rows ref_row0 / cur_row0.
@@ -26,13 +26,21 @@ struct SearchArgs {
   int cost_kind;
   int16_t* mv;
   uint32_t* cost;
+  uint32_t ref_bytes;  // readable bytes from ref (buffer range check), and from cur
+  uint32_t cur_bytes;
 };
 
 struct QsadGeom {
   int tb;          // blocks per workgroup
+  int rows_alloc;  // LDS tile rows (chunks*K + B - 1)
+  int row0;        // first block row of the launch
+  int nrows;       // block rows in the launch
   int groups;      // 4-wide dx groups per block
   int chunks;      // K-row dy chunks
-  int pitch;       // LDS tile row pitch (bytes)
+  int cpp;         // dy chunks per LDS pass
+  int pitch;       // bytes per LDS tile row (multiple of 16)
+  int tile_bytes;  // rows_alloc * pitch
+  uint32_t pitch_magic;  // umulhi(d, pitch_magic) == d / pitch on the staged range
   int threads;     // workgroup size
   int lds;         // dynamic LDS bytes
   int wg_per_row;  // workgroups per block row
@@ -41,7 +49,7 @@ struct QsadGeom {
 };
 
 hipError_t launch_search(const SearchArgs& p, hipStream_t stream, int* used_fast);
-hipError_t launch_generic(const SearchArgs& p, int bx0, int nbx_range, int nrows,
+hipError_t launch_generic(const SearchArgs& p, int bx0, int nbx_range, int row0, int nrows,
                           hipStream_t stream);
 bool plan_qsad(const SearchArgs& p, QsadGeom* g, int* k_out);
 

@@ -23,12 +23,24 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "me_kernels.h"
 
 namespace me {
 
 __device__ __forceinline__ uint64_t make_key(uint32_t cost, int dx, int dy) {
   return ((uint64_t)cost << 32) | ((uint32_t)(dy + 32768) << 16) | (uint32_t)(dx + 32768);
+}
+
+// Compile-time loop: every index is a constant, so register arrays indexed by
+// it never fall back to scratch (plain #pragma unroll gives up on big bodies).
+template <int I, int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
+  }
 }
 
 __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
@@ -51,13 +63,13 @@ __device__ __forceinline__ const uint8_t* row_ptr(const SearchArgs& p, const uin
 // global memory.
 template <int COST>
 __global__ __launch_bounds__(GENERIC_THREADS) void me_generic_kernel(SearchArgs p, int bx0,
-                                                                     int nbx_range,
+                                                                     int nbx_range, int row0,
                                                                      int win_lds_bytes) {
   extern __shared__ __align__(16) uint8_t smem[];
   __shared__ uint64_t red[GENERIC_THREADS / 64];
   const int tid = threadIdx.x;
   const int bx = bx0 + (int)(blockIdx.x % nbx_range);
-  const int by = p.block_row_begin + (int)(blockIdx.x / nbx_range);
+  const int by = row0 + (int)(blockIdx.x / nbx_range);
   const int B = p.blk, S = p.range;
   const int tlx = bx * B, tly = by * B;
   const int w = min(B, p.width - tlx), h = min(B, p.height - tly);
@@ -136,149 +148,356 @@ __global__ __launch_bounds__(GENERIC_THREADS) void me_generic_kernel(SearchArgs 
 }
 
 // --------------------------------------------------------------- qsad (SAD)
-// Workgroup = TB consecutive full-width blocks of one block row.  LDS tile:
-// frame rows [Y0, Y0 + 2S + B) x columns [X0, X0 + pitch), X0 = tlx(b0) - S - a
-// rounded down to a multiple of 4 (a = (tlx - S) mod 4).  Task t of the
-// workgroup -> (dy chunk, block, dx group): the lane evaluates dx offsets
-// q = 4g..4g+3 (dx = q - S - a) and dy offsets d = chunk*K .. +K-1 (dy = d - S).
+// Workgroup = TB consecutive full-width blocks of one block row; the union of
+// their search windows is staged ONCE in LDS:
+//   frame rows [Y0, Y0 + rows_alloc) x columns [X0, X0 + pitch), Y0 = tly - S,
+//   X0 = tlx(b0) - S - a rounded down to a multiple of 4 (a = (tlx - S) mod 4),
+//   zeros outside the frame (those candidates are masked).
+// Each tile row is stored twice, the second copy shifted left by 4 bytes, so
+// every 8-byte qsad operand (ref words w, w+1) is one aligned ds_read_b64 from
+// one copy or the other -- gfx950 needs even-aligned VGPR pairs and unaligned
+// overlapping pairs would cost a v_mov per qsad.
+// Task t of the workgroup -> (dy chunk, block, dx group): the lane owns dx
+// offsets q = 4g..4g+3 (dx = q - S - a) and dy offsets d = chunk*K .. +K-1
+// (dy = d - S); it walks the K + H - 1 window rows once, each row feeding up
+// to K accumulators (u16x4 packed, SAD <= 65280 fits) against the cur block
+// held in VGPRs.
+// Empty volatile asm on the accumulators row YY touched: orders that row's
+// qsads before the next row's (volatile) address step.
+template <int J, int K, int YY, int H>
+__device__ __forceinline__ void pin_rows(uint64_t (&acc)[K]) {
+  if constexpr (J < K) {
+    if constexpr (YY - J >= 0 && YY - J < H) asm volatile("" : "+v"(acc[J]));
+    pin_rows<J + 1, K, YY, H>(acc);
+  }
+}
+
+template <int B, int K, int H>
+__device__ __forceinline__ void qsad_lane(const uint8_t* __restrict__ tile, int pitch,
+                                          uint32_t buf_off, int lrow, int w0,
+                                          const uint32_t (&c)[B][B / 4], uint64_t (&acc)[K]) {
+  constexpr int CW = B / 4;
+  constexpr int NR = K + H - 1;
+  // Operand pair k = ref words (w0 + k, w0 + k + 1) of the current row: one
+  // ds_read2_b32 straight into an aligned VGPR pair.  Pairs 0, 2 come from
+  // byte offset oe = 4*w0, pairs 1, 3 from oo = oe + 4; both advance through
+  // an opaque asm, so the compiler neither hoists every row's address (spills)
+  // nor merges the overlapping words of adjacent pairs (v_mov per qsad).
+  const uint32_t lds0 = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) const uint8_t*)tile);
+  uint32_t oe = lds0 + buf_off + (uint32_t)(lrow * pitch + 4 * w0);
+  uint32_t oo = oe + 4;
+  asm volatile("" : "+v"(oo));
+
+#pragma unroll
+  for (int j = 0; j < K; j++) acc[j] = 0;
+
+  // LDS addresses as plain integers (address space 3, base folded into oe/oo
+  // once) so no per-row add of the dynamic-LDS symbol survives.
+  typedef __attribute__((address_space(3))) const uint32_t lds_u32;
+  auto load = [&](uint64_t (&dst)[CW]) {
+#pragma unroll
+    for (int k = 0; k < CW; k++) {
+      lds_u32* w = reinterpret_cast<lds_u32*>((uintptr_t)((k & 1) ? oo : oe)) + 2 * (k >> 1);
+      dst[k] = ((uint64_t)w[1] << 32) | w[0];
+    }
+  };
+  uint64_t pr[CW], nx[CW];
+  load(pr);
+  static_for<0, NR>([&](auto YY) {
+    constexpr int yy = decltype(YY)::value;
+    // one segment per window row: next row's loads, then this row's qsads.
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (yy + 1 < NR) {
+      oe += pitch;
+      oo += pitch;
+      asm volatile("" : "+v"(oe), "+v"(oo));
+      load(nx);
+    }
+    static_for<0, CW>([&](auto KK) {
+      constexpr int k = decltype(KK)::value;
+      static_for<0, K>([&](auto JJ) {
+        constexpr int j = decltype(JJ)::value;
+        constexpr int y = yy - j;
+        if constexpr (y >= 0 && y < H)
+          acc[j] = __builtin_amdgcn_qsad_pk_u16_u8(pr[k], c[y][k], acc[j]);
+      });
+    });
+    // Pin this row's qsads inside its segment (readnone intrinsics are not
+    // ordered by sched_barrier; the DAG would otherwise sink them past every
+    // later row's loads and spill the loaded rows).
+    pin_rows<0, K, yy, H>(acc);
+    if constexpr (yy + 1 < NR) {
+#pragma unroll
+      for (int k = 0; k < CW; k++) pr[k] = nx[k];
+    }
+  });
+}
+
+#ifdef ME_STAMPS
+// Diagnostic build only (-DME_STAMPS): per-workgroup s_memtime stamps
+// [start, staged, computed, end, hw_id, xcc_id] for tools/stamps.py.
+__device__ unsigned long long g_stamps[8 << 16];
+#define ME_STAMP(slot, v) do { if (threadIdx.x == 0 && wid < (1 << 16)) g_stamps[8 * wid + (slot)] = (v); } while (0)
+#else
+#define ME_STAMP(slot, v) do { } while (0)
+#endif
+
+// 32-bit lane keys (sad << 16 | j*4 + i) ordered like (cost, dy, dx); invalid
+// candidates forced to sad 0xFFFF (> any valid SAD: B*B*255 <= 65280).
+// MASKJ = false on items whose whole dy range is valid (uniform per item).
+template <int K, bool MASKJ>
+__device__ __forceinline__ uint32_t lane_best(const uint64_t (&acc)[K], uint32_t mlo,
+                                              uint32_t mhi, int jlo, int jhi) {
+  uint32_t best = ~0u;
+#pragma unroll
+  for (int j = 0; j < K; j++) {
+    uint32_t lo = (uint32_t)acc[j] | mlo, hi = (uint32_t)(acc[j] >> 32) | mhi;
+    if (MASKJ) {
+      const bool jv = j >= jlo && j <= jhi;
+      lo = jv ? lo : ~0u;
+      hi = jv ? hi : ~0u;
+    }
+    const uint32_t k0 = (lo << 16) | (uint32_t)(4 * j);
+    const uint32_t k1 = (lo & 0xFFFF0000u) | (uint32_t)(4 * j + 1);
+    const uint32_t k2 = (hi << 16) | (uint32_t)(4 * j + 2);
+    const uint32_t k3 = (hi & 0xFFFF0000u) | (uint32_t)(4 * j + 3);
+    best = min(best, min(k0, k1));
+    best = min(best, min(k2, k3));
+  }
+  return best;
+}
+
+// LDS DMA of `bytes` (multiple of 16) into lds_dst: 16 bytes per lane, lane i
+// of DMA step s covers bytes [1024 s + 16 i, +16) of the destination; src_off
+// maps such a destination byte offset to the buffer offset (any uint32: the
+// descriptor's range check returns zeros for offsets past the resident rows,
+// including negative ones, which wrap).
+template <typename F>
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, uint8_t* lds_dst, int bytes,
+                                      F src_off) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int s0 = wave * 1024; s0 < bytes; s0 += nw * 1024) {
+    const int d = s0 + 16 * lane;
+    // lanes past the end must not execute: an out-of-range lane would still
+    // write (zeros) to its LDS slot.
+    if (d < bytes)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rs, (__attribute__((address_space(3))) void*)(lds_dst + s0), 16, src_off(d), 0, 0, 0);
+  }
+}
+
+// LDS DMA with 4-byte granules (256 bytes per wave step): used for the ref
+// tile, whose left/top edges hang off the frame.  X0 is 4-aligned, so no
+// granule straddles x = 0 or x = W (W % 4 == 0 on this path): every granule is
+// either all in-frame or all masked, and the range check zeroes out-of-range
+// ones (a 16-byte granule straddling x = 0 on row 0 would be zeroed whole).
+template <typename F>
+__device__ __forceinline__ void dma4(__amdgpu_buffer_rsrc_t rs, uint8_t* lds_dst, int bytes,
+                                     F src_off) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int s0 = wave * 256; s0 < bytes; s0 += nw * 256) {
+    const int d = s0 + 4 * lane;
+    if (d < bytes)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rs, (__attribute__((address_space(3))) void*)(lds_dst + s0), 4, src_off(d), 0, 0, 0);
+  }
+}
+
+// Geometry of one work item = (tile of TB blocks, dy pass).
+struct Item {
+  int bx0, by, nb, tly, h, a, X0, c0, nch, prow0, prows;
+};
+
+template <int B, int K>
+__device__ __forceinline__ Item item_of(const SearchArgs& p, const QsadGeom& g, int tile,
+                                        int pass) {
+  Item it;
+  it.bx0 = (tile % g.wg_per_row) * g.tb;
+  it.by = g.row0 + tile / g.wg_per_row;
+  it.nb = min(g.tb, g.nbx_full - it.bx0);
+  it.tly = it.by * B;
+  it.h = min(B, p.height - it.tly);
+  it.a = ((it.bx0 * B - p.range) % 4 + 4) % 4;
+  it.X0 = it.bx0 * B - p.range - it.a;
+  it.c0 = pass * g.cpp;
+  it.nch = min(g.cpp, g.chunks - it.c0);
+  it.prow0 = it.tly - p.range + it.c0 * K;  // frame row of tile row 0
+  it.prows = it.nch * K + B - 1;            // rows this item touches
+  return it;
+}
+
+// Issue the staging of one item into an LDS buffer: asynchronous LDS DMA on
+// the aligned path (no VGPR round trip, completes under the previous item's
+// compute), synchronous byte copies otherwise.
+template <int B>
+__device__ __forceinline__ void stage_item(const SearchArgs& p, const QsadGeom& g, const Item& it,
+                                           uint8_t* buf, __amdgpu_buffer_rsrc_t rref,
+                                           __amdgpu_buffer_rsrc_t rcur) {
+  uint8_t* tile = buf;
+  uint8_t* cur = buf + g.tile_bytes;
+  const int pitch = g.pitch, stride = p.stride;
+  const int tid = threadIdx.x, nthr = blockDim.x;
+  if (g.aligned) {
+    // tile byte (r, x) <- ref(prow0 + r, X0 + x); zeros outside the resident rows.
+    const int base = (it.prow0 - p.ref_row0) * stride + it.X0;
+    dma4(rref, tile, it.prows * pitch, [&](int d) {
+      const int r = (int)__umulhi((uint32_t)d, g.pitch_magic), x = d - r * pitch;
+      return (uint32_t)(base + r * stride + x);
+    });
+    // cur block b, row oy -> LDS bytes (b * B + oy) * B
+    const int cbase = (it.tly - p.cur_row0) * stride + it.bx0 * B;
+    if constexpr (B == 16) {
+      dma16(rcur, cur, it.nb * B * B, [&](int d) {
+        return (uint32_t)(cbase + ((d >> 4) & 15) * stride + (d >> 8) * B);
+      });
+    } else {
+      dma4(rcur, cur, it.nb * B * B, [&](int d) {
+        return (uint32_t)(cbase + ((d >> 3) & 7) * stride + (d >> 6) * B + (d & 4));
+      });
+    }
+  } else {
+    for (int i = tid; i < it.prows * pitch; i += nthr) {
+      const int r = i / pitch, x = i - r * pitch;
+      const int y = it.prow0 + r, xx = it.X0 + x;
+      tile[i] = (y >= 0 && y < p.height && xx >= 0 && xx < p.width)
+                    ? row_ptr(p, p.ref, p.ref_row0, y)[xx] : 0;
+    }
+    for (int i = tid; i < it.nb * B * B; i += nthr) {
+      const int b = i / (B * B), rem = i - b * B * B, oy = rem / B, x = rem - oy * B;
+      cur[i] = oy < it.h ? row_ptr(p, p.cur, p.cur_row0, it.tly + oy)[(it.bx0 + b) * B + x] : 0;
+    }
+  }
+}
+
+// Persistent, double-buffered search.  The grid is sized to what fits on the
+// chip at once; workgroups sharing an XCD (bid % 8, a speed heuristic only)
+// walk one contiguous band of tiles, so each XCD's L2 holds one band of rows.
+// Item k of a workgroup = (its k / passes-th tile, pass k % passes); while
+// item k is computed from LDS buffer k & 1, item k + 1 streams into the other.
 template <int B, int K>
 __global__ __launch_bounds__(1024) void me_qsad_kernel(SearchArgs p, QsadGeom g) {
-  constexpr int CW = B / 4;  // cur words per row
+  constexpr int CW = B / 4;
   extern __shared__ __align__(16) uint8_t smem[];
-  uint64_t* keys = reinterpret_cast<uint64_t*>(smem);            // TB keys
-  uint32_t* cur_lds = reinterpret_cast<uint32_t*>(smem + 8 * 16);  // TB * B * CW words
-  uint8_t* tile = smem + 8 * 16 + g.tb * B * B;                     // rows x pitch
+  const int buf_bytes = g.tile_bytes + g.tb * B * B;
+  uint64_t* keys = reinterpret_cast<uint64_t*>(smem + 2 * buf_bytes);
   const int tid = threadIdx.x, nthr = blockDim.x;
   const int S = p.range;
-  const int wg_blocks = g.tb;
-  const int bx0 = (int)(blockIdx.x % g.wg_per_row) * g.tb;
-  const int by = p.block_row_begin + (int)(blockIdx.x / g.wg_per_row);
-  const int nb = min(wg_blocks, g.nbx_full - bx0);
-  const int tly = by * B;
-  const int h = min(B, p.height - tly);
-  const int a = ((bx0 * B - S) % 4 + 4) % 4;
-  const int X0 = bx0 * B - S - a;
-  const int Y0 = tly - S;
-  const int rows = 2 * S + B;
-  const int pw = g.pitch >> 2;
+  const __amdgpu_buffer_rsrc_t rref =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.ref, (short)0, p.ref_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rcur =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.cur, (short)0, p.cur_bytes, 0x00020000);
 
-  if (tid < wg_blocks) keys[tid] = ~0ull;
-  // Stage the ref tile (zeros outside the frame: those candidates are masked).
-  for (int i = tid; i < rows * pw; i += nthr) {
-    const int r = i / pw, q = i - r * pw;
-    const int y = Y0 + r, x = X0 + 4 * q;
-    uint32_t v = 0;
-    if (y >= 0 && y < p.height) {
-      const uint8_t* src = row_ptr(p, p.ref, p.ref_row0, y);
-      if (x >= 0 && x + 3 < p.width && g.aligned) {
-        v = *reinterpret_cast<const uint32_t*>(src + x);
-      } else {
-#pragma unroll
-        for (int k = 0; k < 4; k++)
-          if (x + k >= 0 && x + k < p.width) v |= (uint32_t)src[x + k] << (8 * k);
-      }
-    }
-    reinterpret_cast<uint32_t*>(tile)[i] = v;
-  }
-  // Stage the cur blocks: word (b, oy, k).
-  for (int i = tid; i < nb * B * CW; i += nthr) {
-    const int b = i / (B * CW), rem = i - b * B * CW, oy = rem / CW, k = rem - oy * CW;
-    uint32_t v = 0;
-    if (oy < h) {
-      const uint8_t* src = row_ptr(p, p.cur, p.cur_row0, tly + oy) + (bx0 + b) * B + 4 * k;
-      if (g.aligned) v = *reinterpret_cast<const uint32_t*>(src);
-      else v = src[0] | (src[1] << 8) | (src[2] << 16) | ((uint32_t)src[3] << 24);
-    }
-    cur_lds[i] = v;
-  }
-  __syncthreads();
+  // Tiles of this workgroup: band of XCD group x, member m of n_x.
+  const int ntiles = g.wg_per_row * g.nrows;
+  const int nwg = (int)gridDim.x, bid = (int)blockIdx.x;
+  const int ng = nwg < 8 ? nwg : 8;  // XCD groups that have workgroups
+  const int x = bid % ng, m = bid / ng;
+  const int n_x = nwg / ng + (x < nwg % ng ? 1 : 0);
+  const int band0 = (int)((long)ntiles * x / ng), band1 = (int)((long)ntiles * (x + 1) / ng);
+  const int passes = (g.chunks + g.cpp - 1) / g.cpp;
+  const int my_tiles = band1 - band0 > m ? (band1 - band0 - m + n_x - 1) / n_x : 0;
+  const int nitems = my_tiles * passes;
+  const int wid = bid;
+  ME_STAMP(0, __builtin_amdgcn_s_memtime());
+  ME_STAMP(1, (unsigned long long)nitems);
+  ME_STAMP(6, __builtin_amdgcn_s_memrealtime());
 
+  if (tid < g.tb) keys[tid] = ~0ull;
+  if (nitems > 0) {
+    const Item it0 = item_of<B, K>(p, g, band0 + m, 0);
+    stage_item<B>(p, g, it0, smem, rref, rcur);
+  }
   const int G = g.groups;
-  const int T = nb * G * g.chunks;
-  for (int t = tid; t < T; t += nthr) {
-    const int chunk = t / (nb * G);
-    const int rem = t - chunk * nb * G;
-    const int b = rem / G, gi = rem - b * G;
-    const int d0 = chunk * K;
-
-    uint32_t c[B][CW];
-#pragma unroll
-    for (int y = 0; y < B; y++)
-#pragma unroll
-      for (int k = 0; k < CW; k++) c[y][k] = cur_lds[(b * B + y) * CW + k];
-
-    uint64_t acc[K];
-#pragma unroll
-    for (int j = 0; j < K; j++) acc[j] = 0;
-
-    const uint32_t* rowp = reinterpret_cast<const uint32_t*>(tile) + d0 * pw + (b * B) / 4 + gi;
-    if (h == B) {
-#pragma unroll
-      for (int yy = 0; yy < K + B - 1; yy++) {
-        // rows beyond the tile are only reached by chunk padding (d > 2S):
-        // clamp the address, the candidates are masked below.
-        const int r = min(d0 + yy, rows - 1) - d0;
-        uint32_t wv[CW + 1];
-#pragma unroll
-        for (int k = 0; k <= CW; k++) wv[k] = rowp[r * pw + k];
-#pragma unroll
-        for (int j = 0; j < K; j++) {
-          const int y = yy - j;
-          if (y >= 0 && y < B) {
-#pragma unroll
-            for (int k = 0; k < CW; k++)
-              acc[j] = __builtin_amdgcn_qsad_pk_u16_u8(((uint64_t)wv[k + 1] << 32) | wv[k],
-                                                       c[y][k], acc[j]);
-          }
-        }
-      }
-    } else {
-#pragma unroll
-      for (int yy = 0; yy < K + B - 1; yy++) {
-        const int r = min(d0 + yy, rows - 1) - d0;
-        uint32_t wv[CW + 1];
-#pragma unroll
-        for (int k = 0; k <= CW; k++) wv[k] = rowp[r * pw + k];
-#pragma unroll
-        for (int j = 0; j < K; j++) {
-          const int y = yy - j;
-          if (y >= 0 && y < B && y < h) {
-#pragma unroll
-            for (int k = 0; k < CW; k++)
-              acc[j] = __builtin_amdgcn_qsad_pk_u16_u8(((uint64_t)wv[k + 1] << 32) | wv[k],
-                                                       c[y][k], acc[j]);
-          }
-        }
-      }
+  for (int k = 0; k < nitems; k++) {
+    const int tile_id = band0 + m + (k / passes) * n_x, pass = k % passes;
+    const Item it = item_of<B, K>(p, g, tile_id, pass);
+    uint8_t* buf = smem + (k & 1) * buf_bytes;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // item k staged by every wave; item k-1 fully consumed
+    if (k + 1 < nitems) {
+      const int tn = band0 + m + ((k + 1) / passes) * n_x, pn = (k + 1) % passes;
+      stage_item<B>(p, g, item_of<B, K>(p, g, tn, pn), smem + ((k + 1) & 1) * buf_bytes, rref,
+                    rcur);
     }
+    const uint32_t* cur_lds = reinterpret_cast<const uint32_t*>(buf + g.tile_bytes);
+    const uint32_t tile_off = (uint32_t)((k & 1) * buf_bytes);
+    const int dymin = max(-S, -it.tly), dymax = min(S, p.height - it.h - it.tly);
+    // Chunks whose dy range lies wholly outside [dymin, dymax] (top / bottom
+    // block rows) are skipped: tasks are chunk-major, so whole waves drop out.
+    const int lc0 = max(0, (dymin + S) / K - it.c0);
+    const int lc1 = min(it.nch, (dymax + S) / K + 1 - it.c0);
+    // Every candidate row of this item valid -> no per-row masks (uniform).
+    const bool full_rows = dymin + S <= it.c0 * K && dymax + S >= (it.c0 + it.nch) * K - 1;
+    const int per_chunk = it.nb * G;
+    const int T = (lc1 - lc0) * per_chunk;
+    for (int t = tid; t < T; t += nthr) {
+      const int lc = lc0 + t / per_chunk;
+      const int rem = t - (lc - lc0) * per_chunk;
+      const int b = rem / G, gi = rem - b * G;
+      const int d0 = (it.c0 + lc) * K;
+      const int tlx = (it.bx0 + b) * B;
 
-    // Valid ranges of this block (main.c:73-76 closed form).
-    const int tlx = (bx0 + b) * B;
-    const int dxmin = max(-S, -tlx), dxmax = min(S, p.width - B - tlx);
-    const int dymin = max(-S, -tly), dymax = min(S, p.height - h - tly);
-    uint64_t best = ~0ull;
+      uint32_t c[B][CW];
 #pragma unroll
-    for (int j = 0; j < K; j++) {
-      const int dy = d0 + j - S;
+      for (int y = 0; y < B; y++) {
+        if constexpr (CW == 4) {
+          const uint4 v = reinterpret_cast<const uint4*>(cur_lds)[b * B + y];
+          c[y][0] = v.x; c[y][1] = v.y; c[y][2] = v.z; c[y][3] = v.w;
+        } else {
+          const uint2 v = reinterpret_cast<const uint2*>(cur_lds)[b * B + y];
+          c[y][0] = v.x; c[y][1] = v.y;
+        }
+      }
+      // Valid candidate ranges of this block (main.c:73-76 in closed form).
+      const int dxmin = max(-S, -tlx), dxmax = min(S, p.width - B - tlx);
+      uint32_t mlo = 0, mhi = 0;
 #pragma unroll
       for (int i = 0; i < 4; i++) {
-        const int dx = 4 * gi + i - S - a;
-        const uint32_t sad = (uint32_t)(acc[j] >> (16 * i)) & 0xFFFFu;
-        const bool ok = dx >= dxmin && dx <= dxmax && dy >= dymin && dy <= dymax;
-        const uint64_t key = ok ? make_key(sad, dx, dy) : ~0ull;
-        best = key < best ? key : best;
+        const int dx = 4 * gi + i - S - it.a;
+        const uint32_t msk = (dx < dxmin || dx > dxmax) ? 0xFFFFu : 0u;
+        if (i < 2) mlo |= msk << (16 * i);
+        else mhi |= msk << (16 * (i - 2));
+      }
+      const int jlo = dymin + S - d0, jhi = dymax + S - d0;
+      const int w0 = (b * B) / 4 + gi;
+      uint64_t acc[K];
+      if (it.h == B)
+        qsad_lane<B, K, B>(smem, g.pitch, tile_off, lc * K, w0, c, acc);
+      else
+        qsad_lane<B, K, B / 2>(smem, g.pitch, tile_off, lc * K, w0, c, acc);
+      const uint32_t best = full_rows ? lane_best<K, false>(acc, mlo, mhi, jlo, jhi)
+                                      : lane_best<K, true>(acc, mlo, mhi, jlo, jhi);
+      if (best < 0xFFFF0000u) {
+        const int idx = (int)(best & 0xFFFFu);
+        const int dy = d0 + (idx >> 2) - S, dx = 4 * gi + (idx & 3) - S - it.a;
+        atomicMin(reinterpret_cast<unsigned long long*>(&keys[b]),
+                  (unsigned long long)make_key(best >> 16, dx, dy));
       }
     }
-    atomicMin(reinterpret_cast<unsigned long long*>(&keys[b]), (unsigned long long)best);
+    if (pass == passes - 1) {
+      __syncthreads();  // every task of the tile has folded its key
+      if (tid < it.nb) {
+        const uint64_t kk = keys[tid];
+        keys[tid] = ~0ull;  // ready for this workgroup's next tile
+        const int out = (it.by - p.block_row_begin) * p.nbx + it.bx0 + tid;
+        p.mv[2 * out] = (int16_t)((int)(kk & 0xFFFF) - 32768);
+        p.mv[2 * out + 1] = (int16_t)((int)((kk >> 16) & 0xFFFF) - 32768);
+        if (p.cost) p.cost[out] = (uint32_t)(kk >> 32);
+      }
+    }
   }
-  __syncthreads();
-  if (tid < nb) {
-    const uint64_t k = keys[tid];
-    const int out = (by - p.block_row_begin) * p.nbx + bx0 + tid;
-    p.mv[2 * out] = (int16_t)((int)(k & 0xFFFF) - 32768);
-    p.mv[2 * out + 1] = (int16_t)((int)((k >> 16) & 0xFFFF) - 32768);
-    if (p.cost) p.cost[out] = (uint32_t)(k >> 32);
+  ME_STAMP(2, __builtin_amdgcn_s_memtime());
+#ifdef ME_STAMPS
+  if (tid == 0 && wid < (1 << 16)) {
+    unsigned hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    g_stamps[8 * wid + 3] = __builtin_amdgcn_s_memtime();
+    g_stamps[8 * wid + 4] = hw;
+    g_stamps[8 * wid + 5] = xcc;
+    g_stamps[8 * wid + 7] = __builtin_amdgcn_s_memrealtime();
   }
+#endif
 }
 
 // ------------------------------------------------------------------ launch
@@ -291,16 +510,18 @@ static int generic_lds_bytes(const SearchArgs& p, int* win_bytes) {
   return cur + (int)win;
 }
 
-hipError_t launch_generic(const SearchArgs& p, int bx0, int nbx_range, int nrows,
+hipError_t launch_generic(const SearchArgs& p, int bx0, int nbx_range, int row0, int nrows,
                           hipStream_t stream) {
   if (nbx_range <= 0 || nrows <= 0) return hipSuccess;
   int win = 0;
   const int lds = generic_lds_bytes(p, &win);
   dim3 grid((unsigned)(nbx_range * nrows)), block(GENERIC_THREADS);
   if (p.cost_kind == COST_SAD)
-    hipLaunchKernelGGL(me_generic_kernel<COST_SAD>, grid, block, lds, stream, p, bx0, nbx_range, win);
+    hipLaunchKernelGGL(me_generic_kernel<COST_SAD>, grid, block, lds, stream, p, bx0, nbx_range,
+                       row0, win);
   else
-    hipLaunchKernelGGL(me_generic_kernel<COST_SSD>, grid, block, lds, stream, p, bx0, nbx_range, win);
+    hipLaunchKernelGGL(me_generic_kernel<COST_SSD>, grid, block, lds, stream, p, bx0, nbx_range,
+                       row0, win);
   return hipGetLastError();
 }
 
@@ -312,53 +533,93 @@ bool plan_qsad(const SearchArgs& p, QsadGeom* g, int* k_out) {
   if (S < 1 || S > 255) return false;
   g->nbx_full = p.width / B;
   if (g->nbx_full < 1) return false;
-  static const int Ks_16[] = {13, 11, 8};
-  static const int Ks_8[] = {13, 11, 8};
-  const int* Ks = B == 16 ? Ks_16 : Ks_8;
+  static const int Ks[] = {13, 11, 8};
   const int D = 2 * S + 1;
-  int bestK = Ks[0];
+  int K = Ks[0];
   double bestEff = -1;
-  for (int i = 0; i < 3; i++) {
-    const int K = Ks[i];
-    const int ch = (D + K - 1) / K;
-    const double eff = (double)D / (ch * K);
-    if (eff > bestEff + 1e-9) { bestEff = eff; bestK = K; }
+  for (int k : Ks) {
+    const int ch = (D + k - 1) / k;
+    const double eff = (double)D / (ch * k);
+    if (eff > bestEff + 1e-9) { bestEff = eff; K = k; }
   }
-  const int K = bestK;
   g->chunks = (D + K - 1) / K;
-  // Groups: worst case a = 3 -> ceil((2S + 3 + 1) / 4).
-  g->groups = (2 * S + 3 + 1 + 3) / 4;
-  const int rows = 2 * S + B;
-  int bestTB = 1;
-  double bestUse = -1;
+  g->groups = (2 * S + 3 + 1 + 3) / 4;  // worst case a = 3
+  // Tile row: the words the lanes touch (last block's last group + CW + 1),
+  // padded to 16 bytes (DMA granule) and to an odd number of 16-byte slots so
+  // rows K apart do not map to the same LDS banks.
+  auto pitch_of = [&](int tb) {
+    int pt = (((tb - 1) * B / 4 + g->groups + B / 4 + 1) * 4 + 15) & ~15;
+    if (((pt >> 4) & 1) == 0) pt += 16;
+    return pt;
+  };
+  // (tb, cpp): blocks per workgroup and dy chunks per pass; maximise busy
+  // lanes, then prefer fewer passes.  LDS <= budget keeps >= 2 workgroups/CU.
+  int bestTB = 1, bestC = 1;
+  double bestScore = -1;
   for (int tb = 1; tb <= 16; tb++) {
-    const int width = (tb - 1) * B + 4 * g->groups + 16;
-    const int pitch = (width + 3) & ~3;
-    const long lds = 8 * 16 + (long)tb * B * B + (long)rows * pitch;
-    if (lds > QSAD_LDS_BUDGET) break;
-    const int T = tb * g->groups * g->chunks;
-    const int iters = (T + 1023) / 1024;
-    const int thr = ((T + iters - 1) / iters + 63) & ~63;
-    const double use = (double)T / (iters * thr);
-    // prefer fuller waves; at equal use prefer fewer blocks (more workgroups).
-    if (use > bestUse + 0.02) { bestUse = use; bestTB = tb; }
+    for (int cpp = g->chunks; cpp >= 1; cpp--) {
+      const long lds = 128 + 2 * ((long)tb * B * B + (long)(cpp * K + B - 1) * pitch_of(tb));
+      if (lds > QSAD_LDS_BUDGET) continue;
+      const int passes = (g->chunks + cpp - 1) / cpp;
+      const int T = tb * g->groups * cpp;
+      const int iters = (T + 1023) / 1024;
+      const int thr = ((T + iters - 1) / iters + 63) & ~63;
+      long slots = 0, work = 0;
+      for (int c0 = 0; c0 < g->chunks; c0 += cpp) {
+        const int t = tb * g->groups * (g->chunks - c0 < cpp ? g->chunks - c0 : cpp);
+        slots += (long)((t + thr - 1) / thr) * thr;
+        work += t;
+      }
+      const double score = (double)work / slots - 0.002 * passes;
+      if (score > bestScore + 0.01) { bestScore = score; bestTB = tb; bestC = cpp; }
+    }
   }
   g->tb = bestTB;
-  const int width = (g->tb - 1) * B + 4 * g->groups + 16;
-  g->pitch = (width + 3) & ~3;
-  const int T = g->tb * g->groups * g->chunks;
+  g->cpp = bestC;
+  g->rows_alloc = g->cpp * K + B - 1;
+  g->pitch = pitch_of(g->tb);
+  g->tile_bytes = g->rows_alloc * g->pitch;
+  const int T = g->tb * g->groups * g->cpp;
   const int iters = (T + 1023) / 1024;
   g->threads = ((T + iters - 1) / iters + 63) & ~63;
-  g->lds = 8 * 16 + g->tb * B * B + rows * g->pitch;
+  g->lds = 2 * (g->tile_bytes + g->tb * B * B) + 128;
+  // r = umulhi(d, magic) == d / pitch for every staged offset d (checked).
+  g->pitch_magic = (uint32_t)(0x100000000ull / (uint64_t)g->pitch) + 1u;
+  for (uint32_t d = 0; d < (uint32_t)g->tile_bytes; d += 4)
+    if ((uint32_t)(((uint64_t)d * g->pitch_magic) >> 32) != d / (uint32_t)g->pitch) return false;
   g->wg_per_row = (g->nbx_full + g->tb - 1) / g->tb;
   g->aligned = (p.stride % 4 == 0) && ((uintptr_t)p.ref % 4 == 0) && ((uintptr_t)p.cur % 4 == 0);
   *k_out = K;
   return true;
 }
 
-hipError_t launch_qsad(const SearchArgs& p, const QsadGeom& g, int K, int nrows,
+// Resident workgroups per CU for this kernel / block / LDS (cached per kernel).
+static int resident_wgs(const void* fn, int threads, int lds) {
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, threads, lds) != hipSuccess || n < 1)
+    n = 1;
+  return n;
+}
+
+static int cu_count() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus < 1)
+      cus = 256;
+  }
+  return cus;
+}
+
+hipError_t launch_qsad(const SearchArgs& p, QsadGeom g, int K, int row0, int nrows,
                        hipStream_t stream) {
-  dim3 grid((unsigned)(g.wg_per_row * nrows)), block((unsigned)g.threads);
+  if (nrows <= 0) return hipSuccess;
+  g.row0 = row0;
+  g.nrows = nrows;
+  const int ntiles = g.wg_per_row * nrows;
+  dim3 block((unsigned)g.threads);
 #define ME_QSAD_CASE(BB, KK)                                                              \
   if (p.blk == BB && K == KK) {                                                           \
     if (g.lds > 64 * 1024) {                                                              \
@@ -366,7 +627,9 @@ hipError_t launch_qsad(const SearchArgs& p, const QsadGeom& g, int K, int nrows,
                                           hipFuncAttributeMaxDynamicSharedMemorySize, g.lds); \
       if (e_ != hipSuccess) return e_;                                                    \
     }                                                                                     \
-    hipLaunchKernelGGL((me_qsad_kernel<BB, KK>), grid, block, g.lds, stream, p, g);       \
+    const int res = resident_wgs((const void*)me_qsad_kernel<BB, KK>, g.threads, g.lds);  \
+    const int nwg = ntiles < res * cu_count() ? ntiles : res * cu_count();                \
+    hipLaunchKernelGGL((me_qsad_kernel<BB, KK>), dim3((unsigned)nwg), block, g.lds, stream, p, g); \
     return hipGetLastError();                                                             \
   }
   ME_QSAD_CASE(16, 13) ME_QSAD_CASE(16, 11) ME_QSAD_CASE(16, 8)
@@ -376,20 +639,37 @@ hipError_t launch_qsad(const SearchArgs& p, const QsadGeom& g, int K, int nrows,
 }
 
 hipError_t launch_search(const SearchArgs& p, hipStream_t stream, int* used_fast) {
-  const int nrows = p.block_row_end - p.block_row_begin;
-  if (nrows <= 0) return hipSuccess;
+  const int r0 = p.block_row_begin, r1 = p.block_row_end;
+  if (r1 <= r0) return hipSuccess;
   QsadGeom g;
   int K = 0;
   if (used_fast) *used_fast = 0;
-  if (plan_qsad(p, &g, &K)) {
-    hipError_t e = launch_qsad(p, g, K, nrows, stream);
+  if (!plan_qsad(p, &g, &K)) return launch_generic(p, 0, p.nbx, r0, r1 - r0, stream);
+  // The qsad body is instantiated for full-height blocks and for h = B/2 (the
+  // 1080p bottom row); any other partial bottom row goes to the generic kernel.
+  const int nby = (p.height + p.blk - 1) / p.blk;
+  const int h_last = p.height - (nby - 1) * p.blk;
+  int rq1 = r1;
+  if (r1 == nby && h_last != p.blk && h_last != p.blk / 2) rq1 = r1 - 1;
+  hipError_t e = launch_qsad(p, g, K, r0, rq1 - r0, stream);
+  if (e != hipSuccess) return e;
+  if (used_fast) *used_fast = 1;
+  if (rq1 < r1) {
+    e = launch_generic(p, 0, g.nbx_full, rq1, r1 - rq1, stream);
     if (e != hipSuccess) return e;
-    if (used_fast) *used_fast = 1;
-    if (g.nbx_full < p.nbx)  // partial right column
-      return launch_generic(p, g.nbx_full, p.nbx - g.nbx_full, nrows, stream);
-    return hipSuccess;
   }
-  return launch_generic(p, 0, p.nbx, nrows, stream);
+  if (g.nbx_full < p.nbx)  // partial right column
+    return launch_generic(p, g.nbx_full, p.nbx - g.nbx_full, r0, r1 - r0, stream);
+  return hipSuccess;
 }
 
 }  // namespace me
+
+#ifdef ME_STAMPS
+// Diagnostic build only: copy the per-workgroup stamps to the host.
+extern "C" int me_debug_stamps(unsigned long long* out, int n_words) {
+  if (n_words > (8 << 16)) n_words = 8 << 16;
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(me::g_stamps), (size_t)n_words * 8, 0,
+                                  hipMemcpyDeviceToHost);
+}
+#endif
