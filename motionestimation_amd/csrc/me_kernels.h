@@ -10,7 +10,7 @@ enum { COST_SSD = 0, COST_SAD = 1 };
 
 constexpr int GENERIC_THREADS = 256;
 constexpr int GENERIC_LDS_BUDGET = 60 * 1024;
-constexpr int QSAD_LDS_BUDGET = 80 * 1024;
+constexpr int QSAD_LDS_BUDGET = 40 * 1024;  // 4 workgroups per CU (160 KB LDS)
 
 // One search launch: block rows [block_row_begin, block_row_end) of a
 // width x height frame.  ref / cur point at frame rows ref_row0 / cur_row0.
@@ -51,7 +51,7 @@ struct QsadGeom {
 hipError_t launch_search(const SearchArgs& p, hipStream_t stream, int* used_fast);
 hipError_t launch_generic(const SearchArgs& p, int bx0, int nbx_range, int row0, int nrows,
                           hipStream_t stream);
-bool plan_qsad(const SearchArgs& p, QsadGeom* g, int* k_out);
+bool plan_fast(const SearchArgs& p, QsadGeom* g, int* k_out);
 
 // Consumers of the MV field (me_post.hip).
 hipError_t launch_compensate(const uint8_t* ref, const uint8_t* cur, int width, int height,

@@ -172,6 +172,14 @@ __device__ __forceinline__ void pin_rows(uint64_t (&acc)[K]) {
   }
 }
 
+template <int J, int K, int YY, int H>
+__device__ __forceinline__ void pin_rows32(uint32_t (&acc)[K]) {
+  if constexpr (J < K) {
+    if constexpr (YY - J >= 0 && YY - J < H) asm volatile("" : "+v"(acc[J]));
+    pin_rows32<J + 1, K, YY, H>(acc);
+  }
+}
+
 template <int B, int K, int H>
 __device__ __forceinline__ void qsad_lane(const uint8_t* __restrict__ tile, int pitch,
                                           uint32_t buf_off, int lrow, int w0,
@@ -263,6 +271,83 @@ __device__ __forceinline__ uint32_t lane_best(const uint64_t (&acc)[K], uint32_t
     const uint32_t k3 = (hi & 0xFFFF0000u) | (uint32_t)(4 * j + 3);
     best = min(best, min(k0, k1));
     best = min(best, min(k2, k3));
+  }
+  return best;
+}
+
+// --------------------------------------------------------------- dot4 (SSD)
+// SSD of one dx and K dy candidates, exactly: SSD = sum c^2 + sum r^2 - 2 sum c*r
+// in u32.  sum c*r: v_dot4_u32_u8 of the cur words with the ref words realigned
+// to this lane's dx (v_alignbyte, shift sh); sum r^2: a running prefix P over
+// the window rows (4 more dot4 per row), snapshotted when candidate j's first
+// row arrives (pst[j] = P(j-1)) and closed after its last (pst[j] = P - pst[j]).
+// Returns out[j] = sum r^2 - 2 sum c*r (mod 2^32; the caller adds sum c^2).
+template <int B, int K, int H>
+__device__ __forceinline__ void ssd_lane(const uint8_t* __restrict__ tile, int pitch,
+                                         uint32_t buf_off, int lrow, int wb, int sh,
+                                         const uint32_t (&c)[B][B / 4], uint32_t (&out)[K]) {
+  constexpr int CW = B / 4;
+  constexpr int NR = K + H - 1;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) const uint8_t*)tile);
+  uint32_t o = lds0 + buf_off + (uint32_t)(lrow * pitch + 4 * wb);
+  typedef __attribute__((address_space(3))) const uint32_t lds_u32;
+  auto load = [&](uint32_t (&dst)[CW + 1]) {
+    lds_u32* w = reinterpret_cast<lds_u32*>((uintptr_t)o);
+#pragma unroll
+    for (int k = 0; k <= CW; k++) dst[k] = w[k];
+  };
+  uint32_t acc[K], pst[K];
+#pragma unroll
+  for (int j = 0; j < K; j++) { acc[j] = 0; pst[j] = 0; }
+  uint32_t P = 0;
+  uint32_t w[CW + 1], nw[CW + 1];
+  load(w);
+  static_for<0, NR>([&](auto YY) {
+    constexpr int yy = decltype(YY)::value;
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (yy + 1 < NR) {
+      o += pitch;
+      asm volatile("" : "+v"(o));
+      load(nw);
+    }
+    uint32_t al[CW];
+#pragma unroll
+    for (int k = 0; k < CW; k++) al[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
+    uint32_t rs = 0;
+#pragma unroll
+    for (int k = 0; k < CW; k++) rs = __builtin_amdgcn_udot4(al[k], al[k], rs, false);
+    P += rs;
+    static_for<0, CW>([&](auto KK) {
+      constexpr int k = decltype(KK)::value;
+      static_for<0, K>([&](auto JJ) {
+        constexpr int j = decltype(JJ)::value;
+        constexpr int y = yy - j;
+        if constexpr (y >= 0 && y < H) acc[j] = __builtin_amdgcn_udot4(al[k], c[y][k], acc[j], false);
+      });
+    });
+    if constexpr (yy + 1 < K) pst[yy + 1] = P;          // P(j - 1) for j = yy + 1
+    if constexpr (yy - H + 1 >= 0 && yy - H + 1 < K)    // last row of j = yy - H + 1
+      pst[yy - H + 1] = P - pst[yy - H + 1];
+    pin_rows32<0, K, yy, H>(acc);
+    if constexpr (yy + 1 < NR) {
+#pragma unroll
+      for (int k = 0; k <= CW; k++) w[k] = nw[k];
+    }
+  });
+#pragma unroll
+  for (int j = 0; j < K; j++) out[j] = pst[j] - 2u * acc[j];
+}
+
+// Lane key (ssd << 8 | j): ssd < 2^24 for B <= 16, j < 256.
+template <int K, bool MASKJ>
+__device__ __forceinline__ uint32_t lane_best_ssd(const uint32_t (&v)[K], uint32_t csq,
+                                                  int jlo, int jhi) {
+  uint32_t best = ~0u;
+#pragma unroll
+  for (int j = 0; j < K; j++) {
+    uint32_t key = ((v[j] + csq) << 8) | (uint32_t)j;
+    if (MASKJ) key = (j >= jlo && j <= jhi) ? key : ~0u;
+    best = min(best, key);
   }
   return best;
 }
@@ -374,8 +459,8 @@ __device__ __forceinline__ void stage_item(const SearchArgs& p, const QsadGeom& 
 // walk one contiguous band of tiles, so each XCD's L2 holds one band of rows.
 // Item k of a workgroup = (its k / passes-th tile, pass k % passes); while
 // item k is computed from LDS buffer k & 1, item k + 1 streams into the other.
-template <int B, int K>
-__global__ __launch_bounds__(1024) void me_qsad_kernel(SearchArgs p, QsadGeom g) {
+template <int COST, int B, int K>
+__global__ __launch_bounds__(1024) void me_fast_kernel(SearchArgs p, QsadGeom g) {
   constexpr int CW = B / 4;
   extern __shared__ __align__(16) uint8_t smem[];
   const int buf_bytes = g.tile_bytes + g.tb * B * B;
@@ -450,6 +535,30 @@ __global__ __launch_bounds__(1024) void me_qsad_kernel(SearchArgs p, QsadGeom g)
       }
       // Valid candidate ranges of this block (main.c:73-76 in closed form).
       const int dxmin = max(-S, -tlx), dxmax = min(S, p.width - B - tlx);
+      const int jlo = dymin + S - d0, jhi = dymax + S - d0;
+      if constexpr (COST == COST_SSD) {
+        // lane = one dx (gi = dx + S); its column starts at tile byte b*B + a + gi
+        const int q = b * B + it.a + gi, dx = gi - S;
+        uint32_t csq = 0;
+#pragma unroll
+        for (int y = 0; y < B; y++)
+#pragma unroll
+          for (int kk = 0; kk < CW; kk++) csq = __builtin_amdgcn_udot4(c[y][kk], c[y][kk], csq, false);
+        uint32_t v[K];
+        if (it.h == B)
+          ssd_lane<B, K, B>(smem, g.pitch, tile_off, lc * K, q >> 2, q & 3, c, v);
+        else
+          ssd_lane<B, K, B / 2>(smem, g.pitch, tile_off, lc * K, q >> 2, q & 3, c, v);
+        uint32_t best = full_rows ? lane_best_ssd<K, false>(v, csq, jlo, jhi)
+                                  : lane_best_ssd<K, true>(v, csq, jlo, jhi);
+        if (dx < dxmin || dx > dxmax) best = ~0u;
+        if (best != ~0u) {
+          const int dy = d0 + (int)(best & 0xFFu) - S;
+          atomicMin(reinterpret_cast<unsigned long long*>(&keys[b]),
+                    (unsigned long long)make_key(best >> 8, dx, dy));
+        }
+        continue;
+      }
       uint32_t mlo = 0, mhi = 0;
 #pragma unroll
       for (int i = 0; i < 4; i++) {
@@ -458,7 +567,6 @@ __global__ __launch_bounds__(1024) void me_qsad_kernel(SearchArgs p, QsadGeom g)
         if (i < 2) mlo |= msk << (16 * i);
         else mhi |= msk << (16 * (i - 2));
       }
-      const int jlo = dymin + S - d0, jhi = dymax + S - d0;
       const int w0 = (b * B) / 4 + gi;
       uint64_t acc[K];
       if (it.h == B)
@@ -525,63 +633,68 @@ hipError_t launch_generic(const SearchArgs& p, int bx0, int nbx_range, int row0,
   return hipGetLastError();
 }
 
-// Pick K (dy rows per lane) minimising chunk padding, and TB (blocks per
-// workgroup) minimising idle lanes, within the LDS and 1024-thread limits.
-bool plan_qsad(const SearchArgs& p, QsadGeom* g, int* k_out) {
+// Plan the fast kernels.  SAD lanes own 4 dx (one qsad group), SSD lanes one
+// dx; both own K dy.  Search (K, TB, chunks per pass) for the fewest idle
+// lanes at 256 threads per workgroup (4 workgroups of 4 waves per CU at the
+// kernels' <= 128 VGPRs), within the LDS budget; then prefer fewer passes and
+// smaller tiles (finer work items).
+bool plan_fast(const SearchArgs& p, QsadGeom* g, int* k_out) {
   const int B = p.blk, S = p.range;
-  if (p.cost_kind != COST_SAD || (B != 16 && B != 8)) return false;
+  if (B != 16 && B != 8) return false;
   if (S < 1 || S > 255) return false;
   g->nbx_full = p.width / B;
   if (g->nbx_full < 1) return false;
-  static const int Ks[] = {13, 11, 8};
+  const bool sad = p.cost_kind == COST_SAD;
   const int D = 2 * S + 1;
-  int K = Ks[0];
-  double bestEff = -1;
-  for (int k : Ks) {
-    const int ch = (D + k - 1) / k;
-    const double eff = (double)D / (ch * k);
-    if (eff > bestEff + 1e-9) { bestEff = eff; K = k; }
-  }
-  g->chunks = (D + K - 1) / K;
-  g->groups = (2 * S + 3 + 1 + 3) / 4;  // worst case a = 3
-  // Tile row: the words the lanes touch (last block's last group + CW + 1),
-  // padded to 16 bytes (DMA granule) and to an odd number of 16-byte slots so
-  // rows K apart do not map to the same LDS banks.
-  auto pitch_of = [&](int tb) {
-    int pt = (((tb - 1) * B / 4 + g->groups + B / 4 + 1) * 4 + 15) & ~15;
-    if (((pt >> 4) & 1) == 0) pt += 16;
-    return pt;
-  };
-  // (tb, cpp): blocks per workgroup and dy chunks per pass; maximise busy
-  // lanes, then prefer fewer passes.  LDS <= budget keeps >= 2 workgroups/CU.
-  int bestTB = 1, bestC = 1;
-  double bestScore = -1;
-  for (int tb = 1; tb <= 16; tb++) {
-    for (int cpp = g->chunks; cpp >= 1; cpp--) {
-      const long lds = 128 + 2 * ((long)tb * B * B + (long)(cpp * K + B - 1) * pitch_of(tb));
-      if (lds > QSAD_LDS_BUDGET) continue;
-      const int passes = (g->chunks + cpp - 1) / cpp;
-      const int T = tb * g->groups * cpp;
-      const int iters = (T + 1023) / 1024;
-      const int thr = ((T + iters - 1) / iters + 63) & ~63;
-      long slots = 0, work = 0;
-      for (int c0 = 0; c0 < g->chunks; c0 += cpp) {
-        const int t = tb * g->groups * (g->chunks - c0 < cpp ? g->chunks - c0 : cpp);
-        slots += (long)((t + thr - 1) / thr) * thr;
-        work += t;
+  g->groups = sad ? (2 * S + 3 + 1 + 3) / 4 : D;  // SAD: worst case a = 3
+  static const int Ks[] = {13, 11, 8};
+  const int thr = 256;
+  const int rows = p.block_row_end - p.block_row_begin;
+  double best = -1;
+  int bK = 13, bTB = 1, bC = 1;
+  for (int K : Ks) {
+    const int chunks = (D + K - 1) / K;
+    const double kpad = (double)D / (chunks * K);
+    for (int tb = 1; tb <= 16; tb++) {
+      // bytes the lanes touch per row (+ a <= 3, + alignment word)
+      const int width = (tb - 1) * B + (sad ? 4 * g->groups + B + 4 : 2 * S + 1 + 3 + B + 4);
+      int pt = (width + 15) & ~15;
+      if (((pt >> 4) & 1) == 0) pt += 16;
+      for (int cpp = chunks; cpp >= 1; cpp--) {
+        const long lds = 128 + 2 * ((long)tb * B * B + (long)(cpp * K + B - 1) * pt);
+        if (lds > QSAD_LDS_BUDGET) continue;
+        long slots = 0, work = 0;
+        int passes = 0;
+        for (int c0 = 0; c0 < chunks; c0 += cpp, passes++) {
+          const int t = tb * g->groups * (chunks - c0 < cpp ? chunks - c0 : cpp);
+          slots += (long)((t + thr - 1) / thr) * thr;
+          work += t;
+        }
+        // too few work items leave workgroup slots idle (and nothing to
+        // prefetch): aim for >= 2 items per resident workgroup (4 per CU).
+        const long items = (long)((g->nbx_full + tb - 1) / tb) * rows * passes;
+        const double fill = items >= 2048 ? 1.0 : (double)items / 2048;
+        const double score = kpad * work / slots * (0.7 + 0.3 * fill) - 0.004 * passes - 0.002 * tb;
+        if (score > best + 1e-9) {
+          best = score; bK = K; bTB = tb; bC = cpp;
+          g->pitch = pt;
+        }
       }
-      const double score = (double)work / slots - 0.002 * passes;
-      if (score > bestScore + 0.01) { bestScore = score; bestTB = tb; bestC = cpp; }
     }
   }
-  g->tb = bestTB;
-  g->cpp = bestC;
-  g->rows_alloc = g->cpp * K + B - 1;
-  g->pitch = pitch_of(g->tb);
+  g->tb = bTB;
+  g->cpp = bC;
+  g->chunks = (D + bK - 1) / bK;
+  // recompute the pitch of the chosen tb
+  {
+    const int width = (g->tb - 1) * B + (sad ? 4 * g->groups + B + 4 : 2 * S + 1 + 3 + B + 4);
+    int pt = (width + 15) & ~15;
+    if (((pt >> 4) & 1) == 0) pt += 16;
+    g->pitch = pt;
+  }
+  g->rows_alloc = g->cpp * bK + B - 1;
   g->tile_bytes = g->rows_alloc * g->pitch;
-  const int T = g->tb * g->groups * g->cpp;
-  const int iters = (T + 1023) / 1024;
-  g->threads = ((T + iters - 1) / iters + 63) & ~63;
+  g->threads = thr;
   g->lds = 2 * (g->tile_bytes + g->tb * B * B) + 128;
   // r = umulhi(d, magic) == d / pitch for every staged offset d (checked).
   g->pitch_magic = (uint32_t)(0x100000000ull / (uint64_t)g->pitch) + 1u;
@@ -589,11 +702,11 @@ bool plan_qsad(const SearchArgs& p, QsadGeom* g, int* k_out) {
     if ((uint32_t)(((uint64_t)d * g->pitch_magic) >> 32) != d / (uint32_t)g->pitch) return false;
   g->wg_per_row = (g->nbx_full + g->tb - 1) / g->tb;
   g->aligned = (p.stride % 4 == 0) && ((uintptr_t)p.ref % 4 == 0) && ((uintptr_t)p.cur % 4 == 0);
-  *k_out = K;
+  *k_out = bK;
   return true;
 }
 
-// Resident workgroups per CU for this kernel / block / LDS (cached per kernel).
+// Resident workgroups per CU for this kernel / block / LDS.
 static int resident_wgs(const void* fn, int threads, int lds) {
   int n = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, threads, lds) != hipSuccess || n < 1)
@@ -613,28 +726,30 @@ static int cu_count() {
   return cus;
 }
 
-hipError_t launch_qsad(const SearchArgs& p, QsadGeom g, int K, int row0, int nrows,
+hipError_t launch_fast(const SearchArgs& p, QsadGeom g, int K, int row0, int nrows,
                        hipStream_t stream) {
   if (nrows <= 0) return hipSuccess;
   g.row0 = row0;
   g.nrows = nrows;
   const int ntiles = g.wg_per_row * nrows;
   dim3 block((unsigned)g.threads);
-#define ME_QSAD_CASE(BB, KK)                                                              \
-  if (p.blk == BB && K == KK) {                                                           \
-    if (g.lds > 64 * 1024) {                                                              \
-      hipError_t e_ = hipFuncSetAttribute((const void*)me_qsad_kernel<BB, KK>,            \
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, g.lds); \
-      if (e_ != hipSuccess) return e_;                                                    \
-    }                                                                                     \
-    const int res = resident_wgs((const void*)me_qsad_kernel<BB, KK>, g.threads, g.lds);  \
-    const int nwg = ntiles < res * cu_count() ? ntiles : res * cu_count();                \
-    hipLaunchKernelGGL((me_qsad_kernel<BB, KK>), dim3((unsigned)nwg), block, g.lds, stream, p, g); \
-    return hipGetLastError();                                                             \
+#define ME_FAST_CASE(CC, BB, KK)                                                           \
+  if (p.cost_kind == CC && p.blk == BB && K == KK) {                                       \
+    const void* fn = (const void*)me_fast_kernel<CC, BB, KK>;                              \
+    if (g.lds > 64 * 1024) {                                                               \
+      hipError_t e_ = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, g.lds); \
+      if (e_ != hipSuccess) return e_;                                                     \
+    }                                                                                      \
+    const int res = resident_wgs(fn, g.threads, g.lds);                                    \
+    const int nwg = ntiles < res * cu_count() ? ntiles : res * cu_count();                 \
+    hipLaunchKernelGGL((me_fast_kernel<CC, BB, KK>), dim3((unsigned)nwg), block, g.lds, stream, p, g); \
+    return hipGetLastError();                                                              \
   }
-  ME_QSAD_CASE(16, 13) ME_QSAD_CASE(16, 11) ME_QSAD_CASE(16, 8)
-  ME_QSAD_CASE(8, 13) ME_QSAD_CASE(8, 11) ME_QSAD_CASE(8, 8)
-#undef ME_QSAD_CASE
+  ME_FAST_CASE(COST_SAD, 16, 13) ME_FAST_CASE(COST_SAD, 16, 11) ME_FAST_CASE(COST_SAD, 16, 8)
+  ME_FAST_CASE(COST_SAD, 8, 13) ME_FAST_CASE(COST_SAD, 8, 11) ME_FAST_CASE(COST_SAD, 8, 8)
+  ME_FAST_CASE(COST_SSD, 16, 13) ME_FAST_CASE(COST_SSD, 16, 11) ME_FAST_CASE(COST_SSD, 16, 8)
+  ME_FAST_CASE(COST_SSD, 8, 13) ME_FAST_CASE(COST_SSD, 8, 11) ME_FAST_CASE(COST_SSD, 8, 8)
+#undef ME_FAST_CASE
   return hipErrorInvalidValue;
 }
 
@@ -644,14 +759,14 @@ hipError_t launch_search(const SearchArgs& p, hipStream_t stream, int* used_fast
   QsadGeom g;
   int K = 0;
   if (used_fast) *used_fast = 0;
-  if (!plan_qsad(p, &g, &K)) return launch_generic(p, 0, p.nbx, r0, r1 - r0, stream);
+  if (!plan_fast(p, &g, &K)) return launch_generic(p, 0, p.nbx, r0, r1 - r0, stream);
   // The qsad body is instantiated for full-height blocks and for h = B/2 (the
   // 1080p bottom row); any other partial bottom row goes to the generic kernel.
   const int nby = (p.height + p.blk - 1) / p.blk;
   const int h_last = p.height - (nby - 1) * p.blk;
   int rq1 = r1;
   if (r1 == nby && h_last != p.blk && h_last != p.blk / 2) rq1 = r1 - 1;
-  hipError_t e = launch_qsad(p, g, K, r0, rq1 - r0, stream);
+  hipError_t e = launch_fast(p, g, K, r0, rq1 - r0, stream);
   if (e != hipSuccess) return e;
   if (used_fast) *used_fast = 1;
   if (rq1 < r1) {
