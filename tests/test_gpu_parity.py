@@ -251,3 +251,25 @@ def test_8k_b8_s128_sampled(engine):
             y, x = by * 8, bx * 8
             true_sad = np.abs(c[y:y + 8, x:x + 8] - r[y + 27:y + 35, x - 40:x - 32]).sum()
             assert cost[by * nbx + bx] <= true_sad
+
+
+def test_c_driver_reproduces_published_output(tmp_path, manifest):
+    """bin/mes_hip (C host driver on the ABI, reference argv) writes the
+    reference's published output_4_{7,15}.yuv byte for byte."""
+    import subprocess
+    exe = os.path.join(O.REPO, "bin", "mes_hip")
+    assert os.path.exists(exe), "build with __graft_entry__.build()"
+    f1 = os.path.join(O.GOLDEN, manifest["frames"]["ForemanYF1"]["file"])
+    f4 = os.path.join(O.GOLDEN, manifest["frames"]["ForemanYF4"]["file"])
+    for key, info in manifest["published"].items():
+        r = subprocess.run([exe, f4, f1, str(tmp_path), "4", str(info["span"]), "352", "288",
+                            "--mv", str(tmp_path / "mv.bin")], capture_output=True, text=True,
+                           timeout=120)
+        assert r.returncode == 0, r.stdout + r.stderr
+        out = (tmp_path / f"output_4_{info['span']}.yuv").read_bytes()
+        pub = open(os.path.join(O.GOLDEN, info["file"]), "rb").read()
+        assert out == pub, key
+        assert "Computation time:" in r.stdout
+    r = subprocess.run([exe, f4, f1, str(tmp_path), "8", "12", "352", "288"], capture_output=True,
+                       text=True, timeout=120)
+    assert "PSNR: 31.816000" in r.stdout
