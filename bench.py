@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--cost", choices=["sad", "ssd"], default="sad")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                    help="nccl = RCCL (production); gloo only to rehearse N ranks on one GPU")
     return ap.parse_args()
 
 
@@ -117,10 +119,16 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus != world and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    ndev = torch.cuda.device_count()
+    gpu = local % ndev  # ranks > devices only in a gloo rehearsal on one GPU
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
+    gloo = args.dist_backend == "gloo"
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if gloo:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     import motionestimation_amd as me
     from motionestimation_amd import shard, synth
@@ -129,7 +137,7 @@ def main():
     w, h, seed, sx, sy = synth.CONFIGS[cfg]
     cands_frame = me.candidate_count(w, h, blk, span)
     nb = me.num_blocks(w, h, blk)
-    eng = me.Engine(devices=[local])
+    eng = me.Engine(devices=[gpu])
 
     if args.mode == "frames":
         # rank r: its own frame pair of the sequence (same size; seed varies)
@@ -151,14 +159,15 @@ def main():
         rec = torch.zeros((2, st.max_blocks), dtype=torch.int32, device=dev)
         mv_view = rec[0].view(torch.int16).view(st.max_blocks, 2)
         cost_view = rec[1]
-        bufs = [torch.empty_like(rec) for _ in range(world)] if rank == 0 else None
+        cdev = torch.device("cpu") if gloo else dev
+        bufs = [torch.empty_like(rec, device=cdev) for _ in range(world)] if rank == 0 else None
 
         def step():
             if st.nblocks:
                 eng.search_stripe_device(ref_t, st.ref_y0, cur_t, st.cur_y0, w, h, blk, span,
                                          args.cost, st.row_begin, st.row_end, mv_view, cost_view)
-            if world > 1:
-                dist.gather(rec, bufs, dst=0)
+            if world > 1:  # the one exchange: per-stripe MV records -> rank 0 (RCCL)
+                dist.gather(rec.cpu() if gloo else rec, bufs, dst=0)
         units_per_step = cands_frame
 
     # warmup (untimed)
@@ -184,9 +193,22 @@ def main():
     elapsed = time.perf_counter() - t0
     kern_ms = statistics.mean(a.elapsed_time(b) for a, b in evs)
     if world > 1:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64,
+                         device="cpu" if gloo else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
+
+    parity = None
+    if args.mode == "stripe" and rank == 0 and world > 1:
+        # the gathered field equals a single-GPU full-frame search (not timed)
+        gmv, gcost = shard.assemble(bufs, stripes)
+        fmv = torch.empty((nb, 2), dtype=torch.int16, device=dev)
+        fco = torch.empty(nb, dtype=torch.int32, device=dev)
+        eng.full_search_device(torch.from_numpy(ref).to(dev), torch.from_numpy(cur).to(dev), blk,
+                               span, args.cost, fmv, fco)
+        torch.cuda.synchronize()
+        parity = bool(np.array_equal(gmv, fmv.cpu().numpy()) and
+                      np.array_equal(gcost, fco.cpu().numpy().view(np.uint32)))
 
     value = units_per_step * args.steps / elapsed
     # Roofline of the dominant kernel: algorithmic HBM bytes per
@@ -231,6 +253,8 @@ def main():
                               "frac": absdiffs / (kern_ms / 1e3) / VALU_PEAK_ABSDIFF}},
         "cpu_baseline": None,
     }
+    if parity is not None:
+        line["stripe_gather_parity"] = parity
     if rank == 0 and world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baselines(ref, cur, blk, span, args.cost, args.cpu_threads,
                                              cands_frame)
