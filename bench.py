@@ -175,23 +175,24 @@ def main():
         step()
     torch.cuda.synchronize()
 
-    # kernel duration: HIP events on the stream the search is launched on
-    # (torch's current stream), one pair per step, averaged.
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
+    # Kernel duration: one HIP event pair on the stream the search is launched
+    # on (torch's current stream) around the whole timed region, / K.  Per-step
+    # event pairs would insert a marker between every two launches and stretch
+    # the measured step; the region average is the back-to-back launch time.
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        evs[i][0].record()
+    ev0.record()
+    for _ in range(args.steps):
         step()
-        evs[i][1].record()
+    ev1.record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kern_ms = statistics.mean(a.elapsed_time(b) for a, b in evs)
+    kern_ms = ev0.elapsed_time(ev1) / args.steps
     if world > 1:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64,
                          device="cpu" if gloo else dev)

@@ -41,6 +41,7 @@ struct QsadGeom {
   int pitch;       // bytes per LDS tile row (multiple of 16)
   int tile_bytes;  // rows_alloc * pitch
   uint32_t pitch_magic;  // umulhi(d, pitch_magic) == d / pitch on the staged range
+  uint32_t magic_groups; // umulhi(t, magic_groups) == t / groups on an item's tasks
   int threads;     // workgroup size
   int lds;         // dynamic LDS bytes
   int wg_per_row;  // workgroups per block row

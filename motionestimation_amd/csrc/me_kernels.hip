@@ -515,10 +515,15 @@ __global__ __launch_bounds__(1024) void me_fast_kernel(SearchArgs p, QsadGeom g)
     const bool full_rows = dymin + S <= it.c0 * K && dymax + S >= (it.c0 + it.nch) * K - 1;
     const int per_chunk = it.nb * G;
     const int T = (lc1 - lc0) * per_chunk;
+    // task t -> (chunk, block, group) by multiply-high: t / G with the host's
+    // verified magic, then / nb with a per-item magic (nb <= 16).
+    const uint32_t magic_nb = 0xFFFFFFFFu / (uint32_t)it.nb + 1u;
     for (int t = tid; t < T; t += nthr) {
-      const int lc = lc0 + t / per_chunk;
-      const int rem = t - (lc - lc0) * per_chunk;
-      const int b = rem / G, gi = rem - b * G;
+      const int bg = (int)__umulhi((uint32_t)t, g.magic_groups);  // t / G
+      const int gi = t - bg * G;
+      const int lcr = it.nb == 1 ? bg : (int)__umulhi((uint32_t)bg, magic_nb);  // bg / nb
+      const int b = bg - lcr * it.nb;
+      const int lc = lc0 + lcr;
       const int d0 = (it.c0 + lc) * K;
       const int tlx = (it.bx0 + b) * B;
 
@@ -702,6 +707,16 @@ bool plan_fast(const SearchArgs& p, QsadGeom* g, int* k_out) {
     if ((uint32_t)(((uint64_t)d * g->pitch_magic) >> 32) != d / (uint32_t)g->pitch) return false;
   g->wg_per_row = (g->nbx_full + g->tb - 1) / g->tb;
   g->aligned = (p.stride % 4 == 0) && ((uintptr_t)p.ref % 4 == 0) && ((uintptr_t)p.cur % 4 == 0);
+  // umulhi(t, magic_groups) == t / groups for every task index of an item.
+  g->magic_groups = 0xFFFFFFFFu / (uint32_t)g->groups + 1u;
+  const uint32_t tmax = (uint32_t)(g->tb * g->groups * g->cpp);
+  for (uint32_t t = 0; t < tmax; t++)
+    if ((uint32_t)(((uint64_t)t * g->magic_groups) >> 32) != t / (uint32_t)g->groups) return false;
+  for (uint32_t nb = 1; nb <= (uint32_t)g->tb; nb++) {  // per-item / nb, bg < tb * cpp
+    const uint32_t m = 0xFFFFFFFFu / nb + 1u;
+    for (uint32_t x = 0; x < (uint32_t)(g->tb * g->cpp); x++)
+      if (nb > 1 && (uint32_t)(((uint64_t)x * m) >> 32) != x / nb) return false;
+  }
   *k_out = bK;
   return true;
 }
@@ -740,7 +755,9 @@ hipError_t launch_fast(const SearchArgs& p, QsadGeom g, int K, int row0, int nro
       hipError_t e_ = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, g.lds); \
       if (e_ != hipSuccess) return e_;                                                     \
     }                                                                                      \
-    const int res = resident_wgs(fn, g.threads, g.lds);                                    \
+    thread_local int res_lds = -1, res_n = 1;                                              \
+    if (res_lds != g.lds) { res_n = resident_wgs(fn, g.threads, g.lds); res_lds = g.lds; } \
+    const int res = res_n;                                                                 \
     const int nwg = ntiles < res * cu_count() ? ntiles : res * cu_count();                 \
     hipLaunchKernelGGL((me_fast_kernel<CC, BB, KK>), dim3((unsigned)nwg), block, g.lds, stream, p, g); \
     return hipGetLastError();                                                              \
@@ -753,13 +770,54 @@ hipError_t launch_fast(const SearchArgs& p, QsadGeom g, int K, int row0, int nro
   return hipErrorInvalidValue;
 }
 
+// Plans depend only on the search shape: cache them (per host thread) so a
+// steady stream of same-shape searches pays the planner once.
+struct PlanKey {
+  int width, height, stride, blk, range, cost, rows, aligned;
+  bool operator==(const PlanKey& o) const {
+    return width == o.width && height == o.height && stride == o.stride && blk == o.blk &&
+           range == o.range && cost == o.cost && rows == o.rows && aligned == o.aligned;
+  }
+};
+struct PlanEntry {
+  PlanKey key;
+  bool ok;
+  QsadGeom g;
+  int K;
+};
+
+static bool cached_plan(const SearchArgs& p, QsadGeom* g, int* K) {
+  constexpr int N = 8;
+  thread_local PlanEntry cache[N];
+  thread_local int used = 0, next = 0;
+  const int aligned =
+      (p.stride % 4 == 0) && ((uintptr_t)p.ref % 4 == 0) && ((uintptr_t)p.cur % 4 == 0);
+  const PlanKey key{p.width, p.height, p.stride, p.blk, p.range, p.cost_kind,
+                    p.block_row_end - p.block_row_begin, aligned};
+  for (int i = 0; i < used; i++)
+    if (cache[i].key == key) {
+      *g = cache[i].g;
+      *K = cache[i].K;
+      return cache[i].ok;
+    }
+  PlanEntry e;
+  e.key = key;
+  e.ok = plan_fast(p, &e.g, &e.K);
+  cache[next] = e;
+  next = (next + 1) % N;
+  if (used < N) used++;
+  *g = e.g;
+  *K = e.K;
+  return e.ok;
+}
+
 hipError_t launch_search(const SearchArgs& p, hipStream_t stream, int* used_fast) {
   const int r0 = p.block_row_begin, r1 = p.block_row_end;
   if (r1 <= r0) return hipSuccess;
   QsadGeom g;
   int K = 0;
   if (used_fast) *used_fast = 0;
-  if (!plan_fast(p, &g, &K)) return launch_generic(p, 0, p.nbx, r0, r1 - r0, stream);
+  if (!cached_plan(p, &g, &K)) return launch_generic(p, 0, p.nbx, r0, r1 - r0, stream);
   // The qsad body is instantiated for full-height blocks and for h = B/2 (the
   // 1080p bottom row); any other partial bottom row goes to the generic kernel.
   const int nby = (p.height + p.blk - 1) / p.blk;
