@@ -33,6 +33,7 @@ struct Dev {
   unsigned long long* stats = nullptr;
   uint8_t* out5 = nullptr;
   size_t out_cap = 0;
+  uint32_t* sched = nullptr;  // fast-kernel tile counters (self-resetting)
 };
 
 }  // namespace
@@ -123,6 +124,7 @@ me::SearchArgs make_args(const uint8_t* ref, int ref_row0, const uint8_t* cur, i
   const long ref_rows = ref_end - ref_row0, cur_rows = cur_end - cur_row0;
   p.ref_bytes = ref_rows > 0 ? (uint32_t)((ref_rows - 1) * (long)stride + width) : 0;
   p.cur_bytes = cur_rows > 0 ? (uint32_t)((cur_rows - 1) * (long)stride + width) : 0;
+  p.sched = nullptr;
   return p;
 }
 
@@ -198,6 +200,7 @@ me_status multi_search(me_ctx* c, const uint8_t* ref, const uint8_t* cur, int wi
     uint32_t* dcost = reinterpret_cast<uint32_t*>(d.rec + max_blocks * 4);
     me::SearchArgs p = make_args(d.ref, y_ref0, d.cur, y_cur0, width, height, width, blk, range,
                                  cost, r0, r1, dmv, dcost);
+    p.sched = d.sched;
     HIPCHK(c, me::launch_search(p, d.stream, nullptr));
   }
   Dev& root = c->devs[0];
@@ -324,7 +327,8 @@ me_status me_create(me_ctx** out, const int* device_ids, int n) {
     Dev d;
     d.id = id;
     if (hipSetDevice(id) != hipSuccess ||
-        hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking) != hipSuccess) {
+        hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc((void**)&d.sched, 64) != hipSuccess || hipMemset(d.sched, 0, 64) != hipSuccess) {
       c->devs.push_back(d);
       me_destroy(c);
       (void)hipSetDevice(prev);
@@ -351,6 +355,7 @@ void me_destroy(me_ctx* c) {
     (void)hipFree(d.gather);
     (void)hipFree(d.stats);
     (void)hipFree(d.out5);
+    (void)hipFree(d.sched);
     if (d.stream) (void)hipStreamDestroy(d.stream);
   }
   delete c;
@@ -378,6 +383,7 @@ me_status me_full_search(me_ctx* c, const uint8_t* ref, const uint8_t* cur, int 
   const int nby = (height + blk - 1) / blk;
   me::SearchArgs p = make_args(d.ref, 0, d.cur, 0, width, height, width, blk, range, cost, 0,
                                nby, dmv, dcost);
+  p.sched = d.sched;
   HIPCHK(c, me::launch_search(p, d.stream, nullptr));
   HIPCHK(c, hipMemcpyAsync(mv_xy, dmv, nb * 4, hipMemcpyDeviceToHost, d.stream));
   if (block_cost)
@@ -401,6 +407,7 @@ me_status me_full_search_stripe_device(me_ctx* c, const uint8_t* d_ref, int ref_
   c->err[0] = 0;
   me::SearchArgs p = make_args(d_ref, ref_row0, d_cur, cur_row0, width, height, stride, blk,
                                range, cost, r0, r1, d_mv, d_cost);
+  p.sched = c->devs[0].sched;
   HIPCHK(c, me::launch_search(p, (hipStream_t)stream, nullptr));
   return ME_OK;
 }

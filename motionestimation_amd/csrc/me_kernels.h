@@ -28,6 +28,7 @@ struct SearchArgs {
   uint32_t* cost;
   uint32_t ref_bytes;  // readable bytes from ref (buffer range check), and from cur
   uint32_t cur_bytes;
+  uint32_t* sched;     // 9 zeroed u32 (8 XCD-group tile counters + arrivals) or null
 };
 
 struct QsadGeom {

@@ -472,7 +472,12 @@ __global__ __launch_bounds__(1024) void me_fast_kernel(SearchArgs p, QsadGeom g)
   const __amdgpu_buffer_rsrc_t rcur =
       __builtin_amdgcn_make_buffer_rsrc((void*)p.cur, (short)0, p.cur_bytes, 0x00020000);
 
-  // Tiles of this workgroup: band of XCD group x, member m of n_x.
+  // Tiles of this workgroup come from the band of its XCD group x (bid % 8,
+  // a speed heuristic only).  Dynamic (p.sched != null): the group's
+  // workgroups pull whole tiles from one agent-scope counter, so faster CUs
+  // take more; tile ids are pulled two tiles ahead into an LDS ring so the
+  // double-buffered staging always knows its next item.  Static otherwise:
+  // member m of n_x takes band tiles m, m + n_x, ...
   const int ntiles = g.wg_per_row * g.nrows;
   const int nwg = (int)gridDim.x, bid = (int)blockIdx.x;
   const int ng = nwg < 8 ? nwg : 8;  // XCD groups that have workgroups
@@ -480,30 +485,52 @@ __global__ __launch_bounds__(1024) void me_fast_kernel(SearchArgs p, QsadGeom g)
   const int n_x = nwg / ng + (x < nwg % ng ? 1 : 0);
   const int band0 = (int)((long)ntiles * x / ng), band1 = (int)((long)ntiles * (x + 1) / ng);
   const int passes = (g.chunks + g.cpp - 1) / g.cpp;
-  const int my_tiles = band1 - band0 > m ? (band1 - band0 - m + n_x - 1) / n_x : 0;
-  const int nitems = my_tiles * passes;
+  // Dynamic only with many tiles per workgroup: with few, the two-ahead pulls
+  // hand out every tile at the start (random order) and balance worse than
+  // round-robin; with many, pulls follow CU speed (8K: -7 % time).
+  const bool dyn = p.sched != nullptr && ntiles >= 8 * nwg;
+  int* tq = reinterpret_cast<int*>(smem + 2 * buf_bytes + 128);  // 4-slot ring of tile ids
   const int wid = bid;
   ME_STAMP(0, __builtin_amdgcn_s_memtime());
-  ME_STAMP(1, (unsigned long long)nitems);
   ME_STAMP(6, __builtin_amdgcn_s_memrealtime());
-
-  if (tid < g.tb) keys[tid] = ~0ull;
-  if (nitems > 0) {
-    const Item it0 = item_of<B, K>(p, g, band0 + m, 0);
-    stage_item<B>(p, g, it0, smem, rref, rcur);
+  auto pull = [&]() -> int {
+    const uint32_t i = __hip_atomic_fetch_add(p.sched + x, 1u, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+    return (int)i < band1 - band0 ? band0 + (int)i : -1;
+  };
+  auto tile_at = [&](int i) -> int {  // i-th tile of this workgroup, -1 = none
+    if (dyn) return tq[i & 3];
+    const int t = band0 + m + i * n_x;
+    return t < band1 ? t : -1;
+  };
+  if (dyn && tid == 0) {
+    tq[0] = pull();
+    tq[1] = tq[0] >= 0 ? pull() : -1;
   }
+  if (tid < g.tb) keys[tid] = ~0ull;
+  __syncthreads();
+
+  int ti = 0, pass = 0, nitems = 0;
+  int tile = tile_at(0);
+  if (tile >= 0) stage_item<B>(p, g, item_of<B, K>(p, g, tile, 0), smem, rref, rcur);
   const int G = g.groups;
-  for (int k = 0; k < nitems; k++) {
-    const int tile_id = band0 + m + (k / passes) * n_x, pass = k % passes;
-    const Item it = item_of<B, K>(p, g, tile_id, pass);
+  for (int k = 0; tile >= 0; k++) {
+    const Item it = item_of<B, K>(p, g, tile, pass);
     uint8_t* buf = smem + (k & 1) * buf_bytes;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();  // item k staged by every wave; item k-1 fully consumed
-    if (k + 1 < nitems) {
-      const int tn = band0 + m + ((k + 1) / passes) * n_x, pn = (k + 1) % passes;
-      stage_item<B>(p, g, item_of<B, K>(p, g, tn, pn), smem + ((k + 1) & 1) * buf_bytes, rref,
-                    rcur);
+    if (dyn && pass == 0 && tid == 0) {  // starting tile ti: pull tile ti + 2
+      const int prev = tq[(ti + 1) & 3];
+      tq[(ti + 2) & 3] = prev >= 0 ? pull() : -1;
     }
+    {
+      const int ntile = pass + 1 < passes ? tile : tile_at(ti + 1);
+      const int npass = pass + 1 < passes ? pass + 1 : 0;
+      if (ntile >= 0)
+        stage_item<B>(p, g, item_of<B, K>(p, g, ntile, npass), smem + ((k + 1) & 1) * buf_bytes,
+                      rref, rcur);
+    }
+    nitems++;
     const uint32_t* cur_lds = reinterpret_cast<const uint32_t*>(buf + g.tile_bytes);
     const uint32_t tile_off = (uint32_t)((k & 1) * buf_bytes);
     const int dymin = max(-S, -it.tly), dymax = min(S, p.height - it.h - it.tly);
@@ -597,9 +624,28 @@ __global__ __launch_bounds__(1024) void me_fast_kernel(SearchArgs p, QsadGeom g)
         p.mv[2 * out + 1] = (int16_t)((int)((kk >> 16) & 0xFFFF) - 32768);
         if (p.cost) p.cost[out] = (uint32_t)(kk >> 32);
       }
+      ti++;
+      pass = 0;
+      tile = tile_at(ti);  // written >= one barrier ago
+    } else {
+      pass++;
     }
   }
+  ME_STAMP(1, (unsigned long long)nitems);
   ME_STAMP(2, __builtin_amdgcn_s_memtime());
+  if (dyn && tid == 0) {
+    // The last workgroup out re-zeroes the counters for the next launch on
+    // this stream (every other workgroup's final pull precedes its arrival).
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    const uint32_t d = __hip_atomic_fetch_add(p.sched + 8, 1u, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+    if (d == (uint32_t)nwg - 1) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#pragma unroll
+      for (int i = 0; i < 9; i++)
+        __hip_atomic_store(p.sched + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 #ifdef ME_STAMPS
   if (tid == 0 && wid < (1 << 16)) {
     unsigned hw, xcc;
@@ -700,7 +746,7 @@ bool plan_fast(const SearchArgs& p, QsadGeom* g, int* k_out) {
   g->rows_alloc = g->cpp * bK + B - 1;
   g->tile_bytes = g->rows_alloc * g->pitch;
   g->threads = thr;
-  g->lds = 2 * (g->tile_bytes + g->tb * B * B) + 128;
+  g->lds = 2 * (g->tile_bytes + g->tb * B * B) + 128 + 16;
   // r = umulhi(d, magic) == d / pitch for every staged offset d (checked).
   g->pitch_magic = (uint32_t)(0x100000000ull / (uint64_t)g->pitch) + 1u;
   for (uint32_t d = 0; d < (uint32_t)g->tile_bytes; d += 4)
