@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--config", choices=list(CONFIGS), default="1080p")
     ap.add_argument("--cost", choices=["sad", "ssd"], default="sad")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-stream", action="store_true",
+                    help="skip the host frame-pair streaming leg (PCIe-inclusive, not `value`)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="nccl = RCCL (production); gloo only to rehearse N ranks on one GPU")
@@ -94,6 +96,33 @@ def cpu_baselines(ref, cur, blk, span, cost, threads, cands):
                     "kind": "reference", "cost": "mse",
                     "sample": f"unmodified src/cpu (gcc -O2) on the same frame pair, its own "
                               f"100-thread pool, 'Computation time' median of 3 ({m:.0f} ms)"}
+    return out
+
+
+def host_stream(eng, w, h, blk, span, cost, seed, sx, sy, kern_ms, cands_frame):
+    """Frame-pair streaming from host memory (me_search_pairs):
+    a synthetic pan, consecutive pairs, frames uploaded over PCIe inside the
+    timed call (pinned: direct DMA; pageable: staged), MV records copied back.
+    Reported beside `value`, never as it: `value` has the inputs in HBM."""
+    import motionestimation_amd as me
+    from motionestimation_amd import synth
+    npairs = 16 if w * h <= 2_100_000 else (8 if w * h <= 8_300_000 else 4)
+    pinned = me.pinned_frames(npairs + 1, h, w)
+    synth.sequence(w, h, npairs + 1, seed, sx, sy, out=pinned)
+    pageable = np.array(pinned)
+    pairs = [(k, k + 1) for k in range(npairs)]
+    out = {"pairs": npairs, "workload": f"{npairs + 1}-frame pan, consecutive pairs"}
+    for name, frames in (("pinned", list(pinned)), ("pageable", list(pageable))):
+        eng.search_pairs(frames, pairs, blk, span, cost)  # allocates the device slots
+        reps = 3
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            eng.search_pairs(frames, pairs, blk, span, cost)
+        dt = (time.perf_counter() - t0) / reps
+        out[name] = {"pairs_per_s": npairs / dt, "candidates_per_s": cands_frame * npairs / dt,
+                     "ms_per_pair": dt / npairs * 1e3}
+    out["kernel_only_pairs_per_s"] = 1e3 / kern_ms
+    del pinned
     return out
 
 
@@ -259,6 +288,9 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baselines(ref, cur, blk, span, args.cost, args.cpu_threads,
                                              cands_frame)
+    if rank == 0 and world == 1 and args.mode == "frames" and not args.no_stream:
+        line["host_stream"] = host_stream(eng, w, h, blk, span, args.cost, seed, sx, sy,
+                                          kern_ms, cands_frame)
     if rank == 0:
         print(json.dumps(line), flush=True)
     eng.close()

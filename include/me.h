@@ -53,7 +53,8 @@ typedef enum {
   ME_ENOMEM = 2,      /* host or device allocation failed */
   ME_EDEVICE = 3,     /* HIP runtime / kernel launch error */
   ME_ECOMM = 4,       /* RCCL error in the multi-device gather */
-  ME_EUNSUPPORTED = 5 /* valid request this build cannot serve */
+  ME_EUNSUPPORTED = 5, /* valid request this build cannot serve */
+  ME_EIO = 6           /* file missing, short or malformed (me_yuv_* / me_mv_*) */
 } me_status;
 
 typedef enum {
@@ -158,6 +159,72 @@ me_status me_compensate_planes(me_ctx* ctx, const uint8_t* ref,
                                const uint8_t* cur, int width, int height,
                                int block_size, const int16_t* mv_xy,
                                uint8_t* out5, double* psnr);
+
+/* ---- frame-pair streaming ---- */
+
+/* Pinned (page-locked) host memory.  Frames that live in it are DMAed
+ * straight to the device by me_search_pairs; other frames are staged. */
+void* me_host_alloc(size_t bytes);
+void me_host_free(void* p);
+
+/* Search a list of frame pairs.  frames[0..n_frames) are host Y planes
+ * (width x height, row pitch stride); pairs[2*n], pairs[2*n+1] are the
+ * (ref, cur) frame indices of pair n, e.g. {0,1, 1,2, 2,3} for a sequence or
+ * {0,1, 0,3} for one reference against two currents.  Replaces the
+ * reference's one-pair-per-process driver (src/cpu/main.c:109-179): each
+ * frame is uploaded once per device, the upload of pair n+1's frames overlaps
+ * the search of pair n, and with several context devices the pairs are split
+ * into contiguous runs, one per device (no collective: pairs are
+ * independent).  Results are those of me_full_search on each pair:
+ * mv_xy [n_pairs][nblocks][2], block_cost [n_pairs][nblocks] (may be NULL).
+ * Synchronous. */
+me_status me_search_pairs(me_ctx* ctx, const uint8_t* const* frames, int n_frames,
+                          int width, int height, int stride, int block_size,
+                          int search_range, me_cost cost, const int* pairs,
+                          int n_pairs, int16_t* mv_xy, uint32_t* block_cost);
+
+/* ---- files: u8 YUV planes and the MV-field format ---- */
+
+/* Raw YUV files as the reference reads and writes them (src/common/utils.c:29-92)
+ * but kept in u8 (no int32 widening).  ME_YUV_LUMA: W*H bytes per frame (the
+ * reference's frames/ForemanYF*.yuv); ME_YUV_I420: W*H*3/2 bytes per frame,
+ * luma first. */
+typedef enum { ME_YUV_LUMA = 0, ME_YUV_I420 = 1 } me_yuv_layout;
+
+/* Whole frames in the file, or -1 if it cannot be opened. */
+int64_t me_yuv_frame_count(const char* path, int width, int height, me_yuv_layout layout);
+/* Luma plane of frame `frame_index` into dst (row pitch dst_stride >= width). */
+me_status me_yuv_read_luma(const char* path, int width, int height, me_yuv_layout layout,
+                           int frame_index, uint8_t* dst, int dst_stride);
+/* Write (append != 0: append) `bytes` bytes, e.g. the 5-plane output of
+ * me_compensate_planes (utils.c:75-92 yuvWriteFrame). */
+me_status me_yuv_write(const char* path, const uint8_t* data, size_t bytes, int append);
+
+/* MV-field file, little-endian:
+ *   header (32 B): "MEMV", u16 version = 1, u16 flags (bit 0: costs present),
+ *                  i32 width, height, block_size, search_range, cost, u32 n_pairs
+ *   per pair:      i32 ref_index, i32 cur_index,
+ *                  nblocks x (i16 mvx, i16 mvy)   raster order
+ *                  nblocks x u32 cost             if flags & 1
+ * nblocks = me_num_blocks(width, height, block_size). */
+typedef struct me_mv_header {
+  char magic[4];
+  uint16_t version, flags;
+  int32_t width, height, block_size, search_range, cost;
+  uint32_t n_pairs;
+} me_mv_header;
+
+/* pairs: [n_pairs][2] frame indices (NULL: pair n = (n, n+1));
+ * block_cost may be NULL (flags bit 0 cleared). */
+me_status me_mv_write(const char* path, int width, int height, int block_size,
+                      int search_range, me_cost cost, const int* pairs, int n_pairs,
+                      const int16_t* mv_xy, const uint32_t* block_cost);
+me_status me_mv_read_header(const char* path, me_mv_header* hdr);
+/* Read everything; buffers sized from the header (pairs [n_pairs][2],
+ * mv_xy [n_pairs][nblocks][2], block_cost [n_pairs][nblocks]); any may be
+ * NULL to skip it.  A file without costs leaves block_cost untouched. */
+me_status me_mv_read(const char* path, me_mv_header* hdr, int* pairs, int16_t* mv_xy,
+                     uint32_t* block_cost);
 
 #ifdef __cplusplus
 }

@@ -6,7 +6,9 @@ include/me.h); this package is the host-side mirror of the reference's
 interface over that ABI.  There is no CPU fallback.
 """
 from ._lib import ME_COST_SAD, ME_COST_SSD, MEError, build  # noqa: F401
-from .engine import Engine, candidate_count, num_blocks, plan_stripes, version  # noqa: F401
+from .engine import (Engine, candidate_count, num_blocks, pinned_frames,  # noqa: F401
+                     plan_stripes, version)
+from . import io  # noqa: F401
 from .reference_api import (Block, PredictionFrame, create_prediction_frame,  # noqa: F401
                             find_best_blk_mse, find_best_blks, frame_diff,
                             motion_compensated_frame, output_planes)

@@ -11,7 +11,8 @@ REPO = os.path.dirname(PKG)
 LIB_PATH = os.path.join(PKG, "lib", "libme_hip.so")
 CSRC = os.path.join(PKG, "csrc")
 
-ME_OK, ME_EINVAL, ME_ENOMEM, ME_EDEVICE, ME_ECOMM, ME_EUNSUPPORTED = range(6)
+ME_OK, ME_EINVAL, ME_ENOMEM, ME_EDEVICE, ME_ECOMM, ME_EUNSUPPORTED, ME_EIO = range(7)
+ME_YUV_LUMA, ME_YUV_I420 = 0, 1
 ME_COST_SSD, ME_COST_SAD = 0, 1
 ME_MAX_BLOCK, ME_MAX_RANGE = 64, 1024
 
@@ -40,6 +41,19 @@ _SIGS = {
                              [ctypes.c_void_p, ctypes.c_void_p]),
     "me_compensate_planes": (ctypes.c_int, [ctypes.c_void_p, _u8p, _u8p] + [ctypes.c_int] * 3 +
                              [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)]),
+    "me_host_alloc": (ctypes.c_void_p, [ctypes.c_size_t]),
+    "me_host_free": (None, [ctypes.c_void_p]),
+    "me_search_pairs": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p] + [ctypes.c_int] * 7 +
+                        [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
+    "me_yuv_frame_count": (ctypes.c_int64, [ctypes.c_char_p] + [ctypes.c_int] * 3),
+    "me_yuv_read_luma": (ctypes.c_int, [ctypes.c_char_p] + [ctypes.c_int] * 4 +
+                         [ctypes.c_void_p, ctypes.c_int]),
+    "me_yuv_write": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_size_t,
+                                    ctypes.c_int]),
+    "me_mv_write": (ctypes.c_int, [ctypes.c_char_p] + [ctypes.c_int] * 5 +
+                    [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
+    "me_mv_read_header": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_void_p]),
+    "me_mv_read": (ctypes.c_int, [ctypes.c_char_p] + [ctypes.c_void_p] * 4),
 }
 
 
@@ -51,7 +65,7 @@ class MEError(RuntimeError):
 
 
 _names = {ME_EINVAL: "ME_EINVAL", ME_ENOMEM: "ME_ENOMEM", ME_EDEVICE: "ME_EDEVICE",
-          ME_ECOMM: "ME_ECOMM", ME_EUNSUPPORTED: "ME_EUNSUPPORTED"}
+          ME_ECOMM: "ME_ECOMM", ME_EUNSUPPORTED: "ME_EUNSUPPORTED", ME_EIO: "ME_EIO"}
 
 _lib = None
 

@@ -15,37 +15,11 @@
 #include <new>
 #include <vector>
 
-#include "me.h"
-#include "me_kernels.h"
+#include "me_internal.h"
 
-namespace {
+using me::Dev;
 
-struct Dev {
-  int id = 0;
-  hipStream_t stream = nullptr;
-  uint8_t* ref = nullptr;  // frame (or stripe) planes, packed pitch = width
-  uint8_t* cur = nullptr;
-  size_t frame_cap = 0;
-  uint8_t* rec = nullptr;  // [mv int16 x2 | cost u32] x rec_cap blocks
-  size_t rec_cap = 0;
-  uint8_t* gather = nullptr;  // root only: n_shards * rec bytes
-  size_t gather_cap = 0;
-  unsigned long long* stats = nullptr;
-  uint8_t* out5 = nullptr;
-  size_t out_cap = 0;
-  uint32_t* sched = nullptr;  // fast-kernel tile counters (self-resetting)
-};
-
-}  // namespace
-
-struct me_ctx {
-  std::vector<Dev> devs;
-  bool distinct = true;
-  ncclComm_t* comms = nullptr;
-  char err[512] = {0};
-};
-
-namespace {
+namespace me {
 
 me_status fail(me_ctx* c, me_status s, const char* fmt, ...) {
   if (c) {
@@ -56,22 +30,6 @@ me_status fail(me_ctx* c, me_status s, const char* fmt, ...) {
   }
   return s;
 }
-
-#define HIPCHK(ctx, x)                                                                 \
-  do {                                                                                 \
-    hipError_t e_ = (x);                                                               \
-    if (e_ != hipSuccess)                                                              \
-      return fail(ctx, ME_EDEVICE, "%s:%d %s: %s", __FILE__, __LINE__, #x,             \
-                  hipGetErrorString(e_));                                              \
-  } while (0)
-
-#define NCCLCHK(ctx, x)                                                                \
-  do {                                                                                 \
-    ncclResult_t r_ = (x);                                                             \
-    if (r_ != ncclSuccess)                                                             \
-      return fail(ctx, ME_ECOMM, "%s:%d %s: %s", __FILE__, __LINE__, #x,               \
-                  ncclGetErrorString(r_));                                             \
-  } while (0)
 
 me_status grow(me_ctx* c, void** p, size_t* cap, size_t need) {
   if (*cap >= need && *p) return ME_OK;
@@ -98,10 +56,10 @@ me_status check_args(me_ctx* c, const void* ref, const void* cur, int width, int
   return ME_OK;
 }
 
-me::SearchArgs make_args(const uint8_t* ref, int ref_row0, const uint8_t* cur, int cur_row0,
+SearchArgs make_args(const uint8_t* ref, int ref_row0, const uint8_t* cur, int cur_row0,
                          int width, int height, int stride, int blk, int range, int cost,
                          int r0, int r1, int16_t* mv, uint32_t* cst) {
-  me::SearchArgs p;
+  SearchArgs p;
   p.ref = ref;
   p.cur = cur;
   p.ref_row0 = ref_row0;
@@ -127,6 +85,15 @@ me::SearchArgs make_args(const uint8_t* ref, int ref_row0, const uint8_t* cur, i
   p.sched = nullptr;
   return p;
 }
+
+}  // namespace me
+
+namespace {
+
+using me::fail;
+using me::grow;
+using me::check_args;
+using me::make_args;
 
 uint64_t row_candidates(int width, int height, int blk, int range, int by) {
   const int nbx = (width + blk - 1) / blk;
@@ -254,6 +221,7 @@ const char* me_status_str(me_status s) {
     case ME_EDEVICE: return "device error";
     case ME_ECOMM: return "communication error";
     case ME_EUNSUPPORTED: return "unsupported";
+    case ME_EIO: return "i/o error";
   }
   return "unknown status";
 }
@@ -356,6 +324,7 @@ void me_destroy(me_ctx* c) {
     (void)hipFree(d.stats);
     (void)hipFree(d.out5);
     (void)hipFree(d.sched);
+    me::release_pipeline(d);
     if (d.stream) (void)hipStreamDestroy(d.stream);
   }
   delete c;

@@ -1,0 +1,82 @@
+// me_internal.h -- context internals shared by the C-ABI translation units
+// (me_api.hip: single-frame and stripe entry points; me_stream.hip: frame-pair
+// streaming).  Not installed; include/me.h is the public interface.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <stdarg.h>
+#include <stdint.h>
+
+#include <vector>
+
+#include "me.h"
+#include "me_kernels.h"
+
+namespace me {
+
+struct Dev {
+  int id = 0;
+  hipStream_t stream = nullptr;  // compute stream
+  hipStream_t copy = nullptr;    // upload stream of the pair pipeline (lazy)
+  uint8_t* ref = nullptr;        // frame (or stripe) planes, packed pitch = width
+  uint8_t* cur = nullptr;
+  size_t frame_cap = 0;
+  uint8_t* rec = nullptr;  // [mv int16 x2 | cost u32] x rec_cap blocks
+  size_t rec_cap = 0;
+  uint8_t* gather = nullptr;  // root only: n_shards * rec bytes
+  size_t gather_cap = 0;
+  unsigned long long* stats = nullptr;
+  uint8_t* out5 = nullptr;
+  size_t out_cap = 0;
+  uint32_t* sched = nullptr;  // fast-kernel tile counters (self-resetting)
+  // Frame-pair pipeline (me_stream.hip), kept across calls.
+  std::vector<uint8_t*> slots;        // device frames, slot_bytes each
+  std::vector<hipEvent_t> slot_ready; // upload of the slot's frame done (copy stream)
+  std::vector<hipEvent_t> slot_free;  // last search reading the slot done (compute stream)
+  size_t slot_bytes = 0;
+  uint8_t* stage[2] = {nullptr, nullptr};  // pinned staging for pageable frames
+  hipEvent_t stage_ev[2] = {nullptr, nullptr};
+  size_t stage_bytes = 0;
+  uint8_t* pair_out = nullptr;  // [pairs][nblocks] mv records, then [pairs][nblocks] costs
+  size_t pair_out_cap = 0;
+};
+
+// Free the pair pipeline's buffers and events of one device (me_destroy).
+void release_pipeline(Dev& d);
+
+me_status fail(me_ctx* c, me_status s, const char* fmt, ...);
+me_status grow(me_ctx* c, void** p, size_t* cap, size_t need);
+me_status check_args(me_ctx* c, const void* ref, const void* cur, int width, int height,
+                     int stride, int blk, int range, int cost, const void* mv);
+SearchArgs make_args(const uint8_t* ref, int ref_row0, const uint8_t* cur, int cur_row0,
+                     int width, int height, int stride, int blk, int range, int cost, int r0,
+                     int r1, int16_t* mv, uint32_t* cst);
+
+// Pinned host ranges handed out by me_host_alloc (the pair pipeline DMAs
+// straight from them instead of staging).
+bool host_range_pinned(const void* p, size_t bytes);
+
+}  // namespace me
+
+struct me_ctx {
+  std::vector<me::Dev> devs;
+  bool distinct = true;
+  ncclComm_t* comms = nullptr;
+  char err[512] = {0};
+};
+
+#define HIPCHK(ctx, x)                                                                 \
+  do {                                                                                 \
+    hipError_t e_ = (x);                                                               \
+    if (e_ != hipSuccess)                                                              \
+      return me::fail(ctx, ME_EDEVICE, "%s:%d %s: %s", __FILE__, __LINE__, #x,         \
+                      hipGetErrorString(e_));                                          \
+  } while (0)
+
+#define NCCLCHK(ctx, x)                                                                \
+  do {                                                                                 \
+    ncclResult_t r_ = (x);                                                             \
+    if (r_ != ncclSuccess)                                                             \
+      return me::fail(ctx, ME_ECOMM, "%s:%d %s: %s", __FILE__, __LINE__, #x,           \
+                      ncclGetErrorString(r_));                                         \
+  } while (0)

@@ -490,7 +490,9 @@ __global__ __launch_bounds__(1024) void me_fast_kernel(SearchArgs p, QsadGeom g)
   // round-robin; with many, pulls follow CU speed (8K: -7 % time).
   const bool dyn = p.sched != nullptr && ntiles >= 8 * nwg;
   int* tq = reinterpret_cast<int*>(smem + 2 * buf_bytes + 128);  // 4-slot ring of tile ids
+#ifdef ME_STAMPS
   const int wid = bid;
+#endif
   ME_STAMP(0, __builtin_amdgcn_s_memtime());
   ME_STAMP(6, __builtin_amdgcn_s_memrealtime());
   auto pull = [&]() -> int {
@@ -510,7 +512,10 @@ __global__ __launch_bounds__(1024) void me_fast_kernel(SearchArgs p, QsadGeom g)
   if (tid < g.tb) keys[tid] = ~0ull;
   __syncthreads();
 
-  int ti = 0, pass = 0, nitems = 0;
+  int ti = 0, pass = 0;
+#ifdef ME_STAMPS
+  int nitems = 0;
+#endif
   int tile = tile_at(0);
   if (tile >= 0) stage_item<B>(p, g, item_of<B, K>(p, g, tile, 0), smem, rref, rcur);
   const int G = g.groups;
@@ -530,7 +535,9 @@ __global__ __launch_bounds__(1024) void me_fast_kernel(SearchArgs p, QsadGeom g)
         stage_item<B>(p, g, item_of<B, K>(p, g, ntile, npass), smem + ((k + 1) & 1) * buf_bytes,
                       rref, rcur);
     }
+#ifdef ME_STAMPS
     nitems++;
+#endif
     const uint32_t* cur_lds = reinterpret_cast<const uint32_t*>(buf + g.tile_bytes);
     const uint32_t tile_off = (uint32_t)((k & 1) * buf_bytes);
     const int dymin = max(-S, -it.tly), dymax = min(S, p.height - it.h - it.tly);

@@ -1,0 +1,281 @@
+// me_stream.hip -- frame-pair streaming and pinned host memory.
+//
+// The reference searches one (ref, cur) pair per process (src/cpu/main.c:109-179:
+// read two frames, search, write, exit).  me_search_pairs takes a list of
+// frames and a list of (ref, cur) index pairs -- consecutive pairs of a
+// sequence, or one reference against several currents (the 1->2 and 1->4
+// pairs of frames/ForemanYF{1,2,4}) -- and keeps every device busy:
+//   - each frame is uploaded once per device, into a device slot that lives
+//     from the first to the last pair reading it;
+//   - uploads run on a copy stream, searches on the compute stream; the
+//     host-side staging and upload of pair n+1's new frame overlap the search
+//     of pair n (slots are reused oldest-freed first, so an upload never
+//     waits on the search it should overlap);
+//   - frames in me_host_alloc memory are DMAed directly, other frames are
+//     staged through two pinned buffers;
+//   - MV records stay in HBM until the run ends, then one copy per output.
+// With several context devices the pair list is cut into contiguous runs,
+// one per device, each driven by its own host thread (independent pairs: no
+// collective).
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <deque>
+#include <map>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "me_internal.h"
+
+namespace me {
+
+namespace {
+std::mutex g_pin_mu;
+std::map<uintptr_t, size_t> g_pinned;  // me_host_alloc ranges: base -> bytes
+}  // namespace
+
+bool host_range_pinned(const void* p, size_t bytes) {
+  std::lock_guard<std::mutex> lk(g_pin_mu);
+  const uintptr_t a = (uintptr_t)p;
+  auto it = g_pinned.upper_bound(a);
+  if (it == g_pinned.begin()) return false;
+  --it;
+  return a >= it->first && a + bytes <= it->first + it->second;
+}
+
+void release_pipeline(Dev& d) {
+  if (d.copy) (void)hipStreamSynchronize(d.copy);
+  for (size_t i = 0; i < d.slots.size(); i++) {
+    (void)hipFree(d.slots[i]);
+    (void)hipEventDestroy(d.slot_ready[i]);
+    (void)hipEventDestroy(d.slot_free[i]);
+  }
+  d.slots.clear();
+  d.slot_ready.clear();
+  d.slot_free.clear();
+  d.slot_bytes = 0;
+  for (int k = 0; k < 2; k++) {
+    if (d.stage[k]) (void)hipHostFree(d.stage[k]);
+    if (d.stage_ev[k]) (void)hipEventDestroy(d.stage_ev[k]);
+    d.stage[k] = nullptr;
+    d.stage_ev[k] = nullptr;
+  }
+  d.stage_bytes = 0;
+  (void)hipFree(d.pair_out);
+  d.pair_out = nullptr;
+  d.pair_out_cap = 0;
+  if (d.copy) (void)hipStreamDestroy(d.copy);
+  d.copy = nullptr;
+}
+
+namespace {
+
+struct Job {
+  const uint8_t* const* frames;
+  int n_frames, width, height, stride, blk, range, cost;
+  const int* pairs;
+  int16_t* mv_xy;
+  uint32_t* block_cost;
+};
+
+// Make sure the device's pipeline resources fit this frame size.
+me_status prepare(me_ctx* c, Dev& d, size_t plane) {
+  if (d.slot_bytes != plane) {  // frame size changed: drop the old slots
+    HIPCHK(c, hipStreamSynchronize(d.stream));
+    if (d.copy) HIPCHK(c, hipStreamSynchronize(d.copy));
+    for (size_t i = 0; i < d.slots.size(); i++) {
+      (void)hipFree(d.slots[i]);
+      (void)hipEventDestroy(d.slot_ready[i]);
+      (void)hipEventDestroy(d.slot_free[i]);
+    }
+    d.slots.clear();
+    d.slot_ready.clear();
+    d.slot_free.clear();
+    d.slot_bytes = plane;
+  }
+  if (!d.copy) HIPCHK(c, hipStreamCreateWithFlags(&d.copy, hipStreamNonBlocking));
+  return ME_OK;
+}
+
+me_status new_slot(me_ctx* c, Dev& d, int* idx) {
+  uint8_t* p = nullptr;
+  if (hipMalloc((void**)&p, d.slot_bytes) != hipSuccess)
+    return fail(c, ME_ENOMEM, "hipMalloc(%zu) for a frame slot failed", d.slot_bytes);
+  hipEvent_t r = nullptr, f = nullptr;
+  if (hipEventCreateWithFlags(&r, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&f, hipEventDisableTiming) != hipSuccess) {
+    (void)hipFree(p);
+    if (r) (void)hipEventDestroy(r);
+    return fail(c, ME_EDEVICE, "hipEventCreate failed");
+  }
+  d.slots.push_back(p);
+  d.slot_ready.push_back(r);
+  d.slot_free.push_back(f);
+  *idx = (int)d.slots.size() - 1;
+  return ME_OK;
+}
+
+me_status ensure_staging(me_ctx* c, Dev& d, size_t plane) {
+  if (d.stage_bytes >= plane && d.stage[0]) return ME_OK;
+  for (int k = 0; k < 2; k++) {
+    if (d.stage_ev[k]) HIPCHK(c, hipEventSynchronize(d.stage_ev[k]));
+    if (d.stage[k]) (void)hipHostFree(d.stage[k]);
+    d.stage[k] = nullptr;
+  }
+  d.stage_bytes = 0;
+  for (int k = 0; k < 2; k++) {
+    if (hipHostMalloc((void**)&d.stage[k], plane, hipHostMallocDefault) != hipSuccess)
+      return fail(c, ME_ENOMEM, "pinned staging of %zu bytes failed", plane);
+    if (!d.stage_ev[k]) HIPCHK(c, hipEventCreateWithFlags(&d.stage_ev[k], hipEventDisableTiming));
+  }
+  d.stage_bytes = plane;
+  return ME_OK;
+}
+
+// Pairs [p0, p1) of the job on device d (the calling thread owns d).
+me_status run_pairs(me_ctx* c, Dev& d, const Job& j, int p0, int p1) {
+  if (p1 <= p0) return ME_OK;
+  HIPCHK(c, hipSetDevice(d.id));
+  const int W = j.width, H = j.height, B = j.blk;
+  const size_t plane = (size_t)W * H;
+  const size_t nb = (size_t)me_num_blocks(W, H, B);
+  const int nby = (H + B - 1) / B;
+  me_status s = prepare(c, d, plane);
+  if (s != ME_OK) return s;
+  const size_t np = (size_t)(p1 - p0);
+  if ((s = grow(c, (void**)&d.pair_out, &d.pair_out_cap, np * nb * 8)) != ME_OK) return s;
+  int16_t* out_mv = reinterpret_cast<int16_t*>(d.pair_out);
+  uint32_t* out_cost = reinterpret_cast<uint32_t*>(d.pair_out + np * nb * 4);
+
+  std::vector<int> last_use(j.n_frames, -1), slot_of(j.n_frames, -1);
+  for (int n = p0; n < p1; n++) {
+    last_use[j.pairs[2 * n]] = n;
+    last_use[j.pairs[2 * n + 1]] = n;
+  }
+  std::deque<int> free_slots;  // oldest-freed first
+  for (int i = 0; i < (int)d.slots.size(); i++) free_slots.push_back(i);
+  int stage_k = 0;
+  const size_t span = (size_t)(H - 1) * j.stride + W;
+
+  for (int n = p0; n < p1; n++) {
+    for (int side = 0; side < 2; side++) {
+      const int f = j.pairs[2 * n + side];
+      if (slot_of[f] >= 0) continue;
+      // Keep two freed slots cooling: reusing the slot the previous search
+      // just released would serialise this upload behind that search.
+      int si;
+      if (free_slots.size() < 2) {
+        if ((s = new_slot(c, d, &si)) != ME_OK) return s;
+      } else {
+        si = free_slots.front();
+        free_slots.pop_front();
+        HIPCHK(c, hipStreamWaitEvent(d.copy, d.slot_free[si], 0));
+      }
+      const uint8_t* src = j.frames[f];
+      if (host_range_pinned(src, span)) {
+        HIPCHK(c, hipMemcpy2DAsync(d.slots[si], W, src, j.stride, W, H, hipMemcpyHostToDevice,
+                                   d.copy));
+      } else {
+        if ((s = ensure_staging(c, d, plane)) != ME_OK) return s;
+        // the copy that last read this staging buffer must be done
+        HIPCHK(c, hipEventSynchronize(d.stage_ev[stage_k]));
+        uint8_t* st = d.stage[stage_k];
+        if (j.stride == W) {
+          memcpy(st, src, plane);
+        } else {
+          for (int y = 0; y < H; y++) memcpy(st + (size_t)y * W, src + (size_t)y * j.stride, W);
+        }
+        HIPCHK(c, hipMemcpyAsync(d.slots[si], st, plane, hipMemcpyHostToDevice, d.copy));
+        HIPCHK(c, hipEventRecord(d.stage_ev[stage_k], d.copy));
+        stage_k ^= 1;
+      }
+      HIPCHK(c, hipEventRecord(d.slot_ready[si], d.copy));
+      slot_of[f] = si;
+    }
+    const int sr = slot_of[j.pairs[2 * n]], sc = slot_of[j.pairs[2 * n + 1]];
+    HIPCHK(c, hipStreamWaitEvent(d.stream, d.slot_ready[sr], 0));
+    if (sc != sr) HIPCHK(c, hipStreamWaitEvent(d.stream, d.slot_ready[sc], 0));
+    const size_t o = (size_t)(n - p0) * nb;
+    me::SearchArgs p = make_args(d.slots[sr], 0, d.slots[sc], 0, W, H, W, B, j.range, j.cost, 0,
+                                 nby, out_mv + 2 * o, out_cost + o);
+    p.sched = d.sched;
+    HIPCHK(c, me::launch_search(p, d.stream, nullptr));
+    for (int side = 0; side < 2; side++) {
+      const int f = j.pairs[2 * n + side];
+      if (last_use[f] == n && slot_of[f] >= 0) {
+        const int si = slot_of[f];
+        HIPCHK(c, hipEventRecord(d.slot_free[si], d.stream));
+        free_slots.push_back(si);
+        slot_of[f] = -1;
+      }
+    }
+  }
+  HIPCHK(c, hipMemcpyAsync(j.mv_xy + 2 * nb * p0, out_mv, np * nb * 4, hipMemcpyDeviceToHost,
+                           d.stream));
+  if (j.block_cost)
+    HIPCHK(c, hipMemcpyAsync(j.block_cost + nb * p0, out_cost, np * nb * 4,
+                             hipMemcpyDeviceToHost, d.stream));
+  HIPCHK(c, hipStreamSynchronize(d.stream));
+  return ME_OK;
+}
+
+}  // namespace
+}  // namespace me
+
+extern "C" {
+
+void* me_host_alloc(size_t bytes) {
+  void* p = nullptr;
+  if (bytes == 0 || hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(me::g_pin_mu);
+  me::g_pinned[(uintptr_t)p] = bytes;
+  return p;
+}
+
+void me_host_free(void* p) {
+  if (!p) return;
+  {
+    std::lock_guard<std::mutex> lk(me::g_pin_mu);
+    if (me::g_pinned.erase((uintptr_t)p) == 0) return;  // not ours
+  }
+  (void)hipHostFree(p);
+}
+
+me_status me_search_pairs(me_ctx* c, const uint8_t* const* frames, int n_frames, int width,
+                          int height, int stride, int blk, int range, me_cost cost,
+                          const int* pairs, int n_pairs, int16_t* mv_xy, uint32_t* block_cost) {
+  if (!c) return ME_EINVAL;
+  if (n_pairs < 0 || n_frames < 0) return me::fail(c, ME_EINVAL, "n_pairs %d n_frames %d", n_pairs, n_frames);
+  if (n_pairs == 0) return ME_OK;
+  if (!frames || !pairs) return me::fail(c, ME_EINVAL, "null frames or pairs");
+  for (int n = 0; n < n_pairs; n++)
+    for (int side = 0; side < 2; side++) {
+      const int f = pairs[2 * n + side];
+      if (f < 0 || f >= n_frames) return me::fail(c, ME_EINVAL, "pair %d: frame index %d", n, f);
+      if (!frames[f]) return me::fail(c, ME_EINVAL, "frame %d is null", f);
+    }
+  me_status s = me::check_args(c, frames[pairs[0]], frames[pairs[1]], width, height, stride, blk,
+                               range, cost, mv_xy);
+  if (s != ME_OK) return s;
+  c->err[0] = 0;
+  const me::Job job{frames, n_frames, width, height, stride, blk, range, (int)cost, pairs,
+                    mv_xy, block_cost};
+  const int nd = (int)c->devs.size();
+  if (nd == 1) return me::run_pairs(c, c->devs[0], job, 0, n_pairs);
+  // One host thread per device, contiguous runs of pairs (shared frames of
+  // neighbouring pairs stay on one device); errors land in per-thread contexts.
+  std::vector<me_ctx> errs(nd);
+  std::vector<me_status> st(nd, ME_OK);
+  std::vector<std::thread> th;
+  for (int i = 0; i < nd; i++) {
+    const int p0 = (int)((long)n_pairs * i / nd), p1 = (int)((long)n_pairs * (i + 1) / nd);
+    th.emplace_back([&, i, p0, p1]() { st[i] = me::run_pairs(&errs[i], c->devs[i], job, p0, p1); });
+  }
+  for (auto& t : th) t.join();
+  for (int i = 0; i < nd; i++)
+    if (st[i] != ME_OK) return me::fail(c, st[i], "device %d: %s", c->devs[i].id, errs[i].err);
+  return ME_OK;
+}
+
+}  // extern "C"

@@ -119,6 +119,32 @@ class Engine:
                                               _ptr(mc)), self._h)
         return mc
 
+    def search_pairs(self, frames, pairs, blk: int, span: int, cost="ssd"):
+        """Search many (ref, cur) frame pairs in one pipelined call.
+
+        frames: sequence of (H, W) uint8 planes (or one (N, H, W) array); pairs:
+        [(ref_index, cur_index), ...].  Returns (mv int16 [npairs, nblocks, 2],
+        cost uint32 [npairs, nblocks]).  Frames allocated with
+        :func:`pinned_frames` are DMAed without staging."""
+        # contiguous u8 frames pass through uncopied (pinned ones stay pinned)
+        planes = [np.ascontiguousarray(f, dtype=np.uint8) for f in frames]
+        if not planes:
+            raise MEError(_lib.ME_EINVAL, "no frames")
+        h, w = planes[0].shape
+        for f in planes:
+            if f.shape != (h, w):
+                raise MEError(_lib.ME_EINVAL, f"frame shape {f.shape} != {(h, w)}")
+        pr = np.ascontiguousarray(np.asarray(pairs, dtype=np.int32).reshape(-1, 2))
+        npairs = pr.shape[0]
+        n = num_blocks(w, h, blk) if blk > 0 else 0
+        mv = np.zeros((max(npairs, 1), max(n, 1), 2), np.int16)
+        cst = np.zeros((max(npairs, 1), max(n, 1)), np.uint32)
+        ptrs = (ctypes.c_void_p * len(planes))(*[f.ctypes.data for f in planes])
+        check(_lib.lib().me_search_pairs(self._h, ptrs, len(planes), w, h, w, blk, span,
+                                         cost_code(cost), _ptr(pr), npairs, _ptr(mv),
+                                         _ptr(cst)), self._h)
+        return mv[:npairs, :n], cst[:npairs, :n]
+
     # ----------------------------------------------------------- device API
     def full_search_device(self, ref_t, cur_t, blk: int, span: int, cost, mv_t, cost_t=None,
                            stream=None, width=None, height=None, stride=None):
@@ -141,6 +167,29 @@ class Engine:
             self._h, ref_t.data_ptr(), ref_row0, cur_t.data_ptr(), cur_row0, width, height,
             stride or width, blk, span, cost_code(cost), row_begin, row_end, mv_t.data_ptr(),
             cost_t.data_ptr() if cost_t is not None else None, st), self._h)
+
+
+class _Pinned:
+    """Owner of one me_host_alloc block (freed when the last view dies)."""
+
+    def __init__(self, nbytes: int):
+        self.ptr = _lib.lib().me_host_alloc(nbytes)
+        if not self.ptr:
+            raise MEError(_lib.ME_ENOMEM, f"me_host_alloc({nbytes})")
+
+    def __del__(self):
+        if getattr(self, "ptr", None):
+            _lib.lib().me_host_free(self.ptr)
+            self.ptr = None
+
+
+def pinned_frames(n: int, height: int, width: int) -> np.ndarray:
+    """(n, height, width) uint8 array in pinned host memory (me_host_alloc):
+    frames written here are uploaded by DMA without a staging copy."""
+    owner = _Pinned(max(1, n * height * width))
+    buf = (ctypes.c_uint8 * (n * height * width)).from_address(owner.ptr)
+    buf._owner = owner  # keep the allocation alive with every view
+    return np.frombuffer(buf, dtype=np.uint8).reshape(n, height, width)
 
 
 def _current_stream():

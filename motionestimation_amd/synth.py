@@ -64,3 +64,22 @@ def frame_pair(width: int, height: int, seed: int, shift_x: int, shift_y: int):
 def named_pair(name: str):
     w, h, seed, sx, sy = CONFIGS[name]
     return frame_pair(w, h, seed, sx, sy)
+
+
+def sequence(width: int, height: int, n: int, seed: int, step_x: int, step_y: int,
+             out: np.ndarray | None = None) -> np.ndarray:
+    """n frames (n, height, width): frame k = the seed's box-filtered plane
+    displaced by (k*step_x, k*step_y) plus its own [-2, 2] noise (stream k+1) --
+    a camera pan for the frame-pair streaming path.  Written into `out` if given
+    (e.g. pinned host memory)."""
+    npx = width * height
+    noise = (splitmix64(seed, npx, 0) >> np.uint64(56)).astype(np.uint8).reshape(height, width)
+    base = _box5(noise)
+    if out is None:
+        out = np.empty((n, height, width), np.uint8)
+    for k in range(n):
+        jitter = (splitmix64(seed, npx, k + 1) % np.uint64(5)).astype(np.int16).reshape(
+            height, width) - 2
+        out[k] = np.clip(shift_plane(base, k * step_x, k * step_y).astype(np.int16) + jitter,
+                         0, 255).astype(np.uint8)
+    return out

@@ -270,6 +270,11 @@ def test_c_driver_reproduces_published_output(tmp_path, manifest):
         pub = open(os.path.join(O.GOLDEN, info["file"]), "rb").read()
         assert out == pub, key
         assert "Computation time:" in r.stdout
+        hdr, pairs, mv, cost = me.io.read_mv(tmp_path / "mv.bin")
+        assert (hdr["block_size"], hdr["search_range"], hdr["n_pairs"]) == (4, info["span"], 1)
+        gmv, _ = O.load_case([c for c in manifest["cases"]
+                              if c["name"] == f"foreman41_b4_s{info['span']}"][0])
+        np.testing.assert_array_equal(mv[0].astype(np.int32), gmv)
     r = subprocess.run([exe, f4, f1, str(tmp_path), "8", "12", "352", "288"], capture_output=True,
                        text=True, timeout=120)
     assert "PSNR: 31.816000" in r.stdout

@@ -8,7 +8,7 @@
  * (main.c:160-178) by me_compensate_planes().  Extra trailing options:
  *   --cost ssd|sad      (default ssd = the reference's MSE choice)
  *   --gpus N            stripe the search over devices 0..N-1 (RCCL gather)
- *   --mv FILE           MV dump: int16 (mvx, mvy) + uint32 cost per block
+ *   --mv FILE           MV field + costs as a MEMV file (include/me.h, me_mv_write)
  * Errors print a message and return 1 (no exit() inside the library).
  */
 #include <stdio.h>
@@ -106,23 +106,10 @@ int main(int argc, char** argv) {
   printf("Output file dimensions: (%d x %d)\n", W, 5 * H);
   char path[4096];
   snprintf(path, sizeof path, "%s/output_%d_%d.yuv", pos[2], blk, span);
-  FILE* f = fopen(path, "wb");
-  if (f) {
-    fwrite(out, 1, 5 * n, f);
-    fclose(f);
-  } else {
+  if (me_yuv_write(path, out, 5 * n, 0) != ME_OK)
     printf("yuvWriteToFile: Could not open the file %s\n", path);
-  }
-  if (mv_path) {
-    FILE* g = fopen(mv_path, "wb");
-    if (g) {
-      for (int i = 0; i < nb; i++) {
-        fwrite(&mv[2 * i], sizeof(int16_t), 2, g);
-        fwrite(&bc[i], sizeof(uint32_t), 1, g);
-      }
-      fclose(g);
-    }
-  }
+  if (mv_path && me_mv_write(mv_path, W, H, blk, span, cost, NULL, 1, mv, bc) != ME_OK)
+    printf("Error: could not write %s\n", mv_path);
   printf("Computation time: %.lf ms\n", (t1 - t0) * 1000);
   printf("PSNR: %.lf \n", psnr);
   me_destroy(ctx);
