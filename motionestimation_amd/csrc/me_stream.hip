@@ -174,8 +174,11 @@ me_status run_pairs(me_ctx* c, Dev& d, const Job& j, int p0, int p1) {
       }
       const uint8_t* src = j.frames[f];
       if (host_range_pinned(src, span)) {
-        HIPCHK(c, hipMemcpy2DAsync(d.slots[si], W, src, j.stride, W, H, hipMemcpyHostToDevice,
-                                   d.copy));
+        if (j.stride == W)
+          HIPCHK(c, hipMemcpyAsync(d.slots[si], src, plane, hipMemcpyHostToDevice, d.copy));
+        else
+          HIPCHK(c, hipMemcpy2DAsync(d.slots[si], W, src, j.stride, W, H, hipMemcpyHostToDevice,
+                                     d.copy));
       } else {
         if ((s = ensure_staging(c, d, plane)) != ME_OK) return s;
         // the copy that last read this staging buffer must be done
