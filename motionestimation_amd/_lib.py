@@ -9,6 +9,10 @@ import subprocess
 PKG = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(PKG)
 LIB_PATH = os.path.join(PKG, "lib", "libme_hip.so")
+# Diagnostic builds only (tools/ablate.sh, tools/stamps.py): another in-tree
+# build of the same library.
+if os.environ.get("ME_HIP_LIB"):
+    LIB_PATH = os.path.join(PKG, "lib", os.path.basename(os.environ["ME_HIP_LIB"]))
 CSRC = os.path.join(PKG, "csrc")
 
 ME_OK, ME_EINVAL, ME_ENOMEM, ME_EDEVICE, ME_ECOMM, ME_EUNSUPPORTED, ME_EIO = range(7)

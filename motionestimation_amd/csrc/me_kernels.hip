@@ -22,10 +22,16 @@
 //                          even when the float sum rounds.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
 
 #include <type_traits>
 
 #include "me_kernels.h"
+
+#ifndef ME_ABLATE
+#define ME_ABLATE 0  // diagnostic builds only (csrc/Makefile ablate); never shipped
+#endif
 
 namespace me {
 
@@ -226,8 +232,12 @@ __device__ __forceinline__ void qsad_lane(const uint8_t* __restrict__ tile, int 
       static_for<0, K>([&](auto JJ) {
         constexpr int j = decltype(JJ)::value;
         constexpr int y = yy - j;
+#if ME_ABLATE == 2  // diagnostic: everything but the qsad issue cost
+        if constexpr (y >= 0 && y < H) acc[j] ^= (uint32_t)pr[k] ^ c[y][k];
+#else
         if constexpr (y >= 0 && y < H)
           acc[j] = __builtin_amdgcn_qsad_pk_u16_u8(pr[k], c[y][k], acc[j]);
+#endif
       });
     });
     // Pin this row's qsads inside its segment (readnone intrinsics are not
@@ -256,7 +266,10 @@ __device__ unsigned long long g_stamps[8 << 16];
 template <int K, bool MASKJ>
 __device__ __forceinline__ uint32_t lane_best(const uint64_t (&acc)[K], uint32_t mlo,
                                               uint32_t mhi, int jlo, int jhi) {
-  uint32_t best = ~0u;
+  // Two independent min3 chains (i = 0,1 and i = 2,3): the epilogues of all
+  // waves on a SIMD tend to coincide (item barriers), so a single 2K-deep
+  // dependent chain would run at VALU latency, not issue rate.
+  uint32_t b01 = ~0u, b23 = ~0u;
 #pragma unroll
   for (int j = 0; j < K; j++) {
     uint32_t lo = (uint32_t)acc[j] | mlo, hi = (uint32_t)(acc[j] >> 32) | mhi;
@@ -269,10 +282,10 @@ __device__ __forceinline__ uint32_t lane_best(const uint64_t (&acc)[K], uint32_t
     const uint32_t k1 = (lo & 0xFFFF0000u) | (uint32_t)(4 * j + 1);
     const uint32_t k2 = (hi << 16) | (uint32_t)(4 * j + 2);
     const uint32_t k3 = (hi & 0xFFFF0000u) | (uint32_t)(4 * j + 3);
-    best = min(best, min(k0, k1));
-    best = min(best, min(k2, k3));
+    b01 = min(b01, min(k0, k1));
+    b23 = min(b23, min(k2, k3));
   }
-  return best;
+  return min(b01, b23);
 }
 
 // --------------------------------------------------------------- dot4 (SSD)
@@ -338,18 +351,25 @@ __device__ __forceinline__ void ssd_lane(const uint8_t* __restrict__ tile, int p
   for (int j = 0; j < K; j++) out[j] = pst[j] - 2u * acc[j];
 }
 
-// Lane key (ssd << 8 | j): ssd < 2^24 for B <= 16, j < 256.
+// Lane key ((v + SSD_BIAS) << 5 | j) with v = sum r^2 - 2 sum c*r: SSD = v +
+// sum c^2, and sum c^2 is the same for every candidate of a block, so v ranks
+// them exactly; v >= -sum c^2 > -2^24 (B <= 16), so v + SSD_BIAS lies in
+// [0, 2^25) and the key below 2^30 (j < 32).  Block costs get sum c^2 back
+// once per block at output.
+constexpr uint32_t SSD_BIAS = 1u << 24;
+
 template <int K, bool MASKJ>
-__device__ __forceinline__ uint32_t lane_best_ssd(const uint32_t (&v)[K], uint32_t csq,
-                                                  int jlo, int jhi) {
-  uint32_t best = ~0u;
+__device__ __forceinline__ uint32_t lane_best_ssd(const uint32_t (&v)[K], int jlo, int jhi) {
+  static_assert(K < 32, "j field is 5 bits");
+  uint32_t b0 = ~0u, b1 = ~0u;  // two chains (see lane_best)
 #pragma unroll
   for (int j = 0; j < K; j++) {
-    uint32_t key = ((v[j] + csq) << 8) | (uint32_t)j;
+    uint32_t key = ((v[j] + SSD_BIAS) << 5) | (uint32_t)j;
     if (MASKJ) key = (j >= jlo && j <= jhi) ? key : ~0u;
-    best = min(best, key);
+    if (j & 1) b1 = min(b1, key);
+    else b0 = min(b0, key);
   }
-  return best;
+  return min(b0, b1);
 }
 
 // LDS DMA of `bytes` (multiple of 16) into lds_dst: 16 bytes per lane, lane i
@@ -578,33 +598,20 @@ __global__ __launch_bounds__(1024) void me_fast_kernel(SearchArgs p, QsadGeom g)
       if constexpr (COST == COST_SSD) {
         // lane = one dx (gi = dx + S); its column starts at tile byte b*B + a + gi
         const int q = b * B + it.a + gi, dx = gi - S;
-        uint32_t csq = 0;
-#pragma unroll
-        for (int y = 0; y < B; y++)
-#pragma unroll
-          for (int kk = 0; kk < CW; kk++) csq = __builtin_amdgcn_udot4(c[y][kk], c[y][kk], csq, false);
         uint32_t v[K];
         if (it.h == B)
           ssd_lane<B, K, B>(smem, g.pitch, tile_off, lc * K, q >> 2, q & 3, c, v);
         else
           ssd_lane<B, K, B / 2>(smem, g.pitch, tile_off, lc * K, q >> 2, q & 3, c, v);
-        uint32_t best = full_rows ? lane_best_ssd<K, false>(v, csq, jlo, jhi)
-                                  : lane_best_ssd<K, true>(v, csq, jlo, jhi);
+        uint32_t best = full_rows ? lane_best_ssd<K, false>(v, jlo, jhi)
+                                  : lane_best_ssd<K, true>(v, jlo, jhi);
         if (dx < dxmin || dx > dxmax) best = ~0u;
         if (best != ~0u) {
-          const int dy = d0 + (int)(best & 0xFFu) - S;
+          const int dy = d0 + (int)(best & 31u) - S;
           atomicMin(reinterpret_cast<unsigned long long*>(&keys[b]),
-                    (unsigned long long)make_key(best >> 8, dx, dy));
+                    (unsigned long long)make_key(best >> 5, dx, dy));
         }
         continue;
-      }
-      uint32_t mlo = 0, mhi = 0;
-#pragma unroll
-      for (int i = 0; i < 4; i++) {
-        const int dx = 4 * gi + i - S - it.a;
-        const uint32_t msk = (dx < dxmin || dx > dxmax) ? 0xFFFFu : 0u;
-        if (i < 2) mlo |= msk << (16 * i);
-        else mhi |= msk << (16 * (i - 2));
       }
       const int w0 = (b * B) / 4 + gi;
       uint64_t acc[K];
@@ -612,9 +619,35 @@ __global__ __launch_bounds__(1024) void me_fast_kernel(SearchArgs p, QsadGeom g)
         qsad_lane<B, K, B>(smem, g.pitch, tile_off, lc * K, w0, c, acc);
       else
         qsad_lane<B, K, B / 2>(smem, g.pitch, tile_off, lc * K, w0, c, acc);
-      const uint32_t best = full_rows ? lane_best<K, false>(acc, mlo, mhi, jlo, jhi)
-                                      : lane_best<K, true>(acc, mlo, mhi, jlo, jhi);
+      // Waves with no frame-edge candidate (most of them) take the unmasked
+      // epilogue: the test is wave-uniform, so there is no divergence.
+      const int dxg = 4 * gi - S - it.a;  // dx of this lane's first candidate
+      const bool edge = dxg < dxmin || dxg + 3 > dxmax;
+      uint32_t best;
+#if ME_ABLATE == 1  // diagnostic: no epilogue
+      if (true) {
+        best = (uint32_t)(acc[0] ^ acc[K - 1]) & 0xFFFF0000u;
+        (void)edge;
+      } else
+#endif
+      if (full_rows && __builtin_amdgcn_ballot_w64(edge) == 0) {
+        best = lane_best<K, false>(acc, 0u, 0u, jlo, jhi);
+      } else {
+        uint32_t mlo = 0, mhi = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          const int dx = dxg + i;
+          const uint32_t msk = (dx < dxmin || dx > dxmax) ? 0xFFFFu : 0u;
+          if (i < 2) mlo |= msk << (16 * i);
+          else mhi |= msk << (16 * (i - 2));
+        }
+        best = lane_best<K, true>(acc, mlo, mhi, jlo, jhi);
+      }
+#if ME_ABLATE == 3  // diagnostic: no key atomics
+      if (best == 0x12345u) {
+#else
       if (best < 0xFFFF0000u) {
+#endif
         const int idx = (int)(best & 0xFFFFu);
         const int dy = d0 + (idx >> 2) - S, dx = 4 * gi + (idx & 3) - S - it.a;
         atomicMin(reinterpret_cast<unsigned long long*>(&keys[b]),
@@ -629,7 +662,15 @@ __global__ __launch_bounds__(1024) void me_fast_kernel(SearchArgs p, QsadGeom g)
         const int out = (it.by - p.block_row_begin) * p.nbx + it.bx0 + tid;
         p.mv[2 * out] = (int16_t)((int)(kk & 0xFFFF) - 32768);
         p.mv[2 * out + 1] = (int16_t)((int)((kk >> 16) & 0xFFFF) - 32768);
-        if (p.cost) p.cost[out] = (uint32_t)(kk >> 32);
+        uint32_t cost = (uint32_t)(kk >> 32);
+        if constexpr (COST == COST_SSD) {  // biased v -> SSD: + sum c^2 of the block
+          const uint32_t* cb = reinterpret_cast<const uint32_t*>(buf + g.tile_bytes) + tid * B * CW;
+          uint32_t csq = 0;
+#pragma unroll 4
+          for (int i = 0; i < B * CW; i++) csq = __builtin_amdgcn_udot4(cb[i], cb[i], csq, false);
+          cost = cost - SSD_BIAS + csq;
+        }
+        if (p.cost) p.cost[out] = cost;
       }
       ti++;
       pass = 0;
@@ -706,19 +747,30 @@ bool plan_fast(const SearchArgs& p, QsadGeom* g, int* k_out) {
   const int D = 2 * S + 1;
   g->groups = sad ? (2 * S + 3 + 1 + 3) / 4 : D;  // SAD: worst case a = 3
   static const int Ks[] = {13, 11, 8};
-  const int thr = 256;
+  // Tuning override (tools/plan_sweep.py only): ME_PLAN="K,tb,cpp,threads",
+  // 0 = free; read once per process.
+  static int force[4] = {-1, 0, 0, 0};
+  if (force[0] < 0) {
+    force[0] = 0;
+    if (const char* e = getenv("ME_PLAN"))
+      sscanf(e, "%d,%d,%d,%d", &force[0], &force[1], &force[2], &force[3]);
+  }
+  const int thr = force[3] > 0 ? force[3] : 256;
   const int rows = p.block_row_end - p.block_row_begin;
   double best = -1;
   int bK = 13, bTB = 1, bC = 1;
   for (int K : Ks) {
+    if (force[0] && K != force[0]) continue;
     const int chunks = (D + K - 1) / K;
     const double kpad = (double)D / (chunks * K);
     for (int tb = 1; tb <= 16; tb++) {
+      if (force[1] && tb != force[1]) continue;
       // bytes the lanes touch per row (+ a <= 3, + alignment word)
       const int width = (tb - 1) * B + (sad ? 4 * g->groups + B + 4 : 2 * S + 1 + 3 + B + 4);
       int pt = (width + 15) & ~15;
       if (((pt >> 4) & 1) == 0) pt += 16;
       for (int cpp = chunks; cpp >= 1; cpp--) {
+        if (force[2] && cpp != force[2]) continue;
         const long lds = 128 + 2 * ((long)tb * B * B + (long)(cpp * K + B - 1) * pt);
         if (lds > QSAD_LDS_BUDGET) continue;
         long slots = 0, work = 0;
@@ -740,6 +792,7 @@ bool plan_fast(const SearchArgs& p, QsadGeom* g, int* k_out) {
       }
     }
   }
+  if (best < 0) return false;  // nothing fits (only with an ME_PLAN override)
   g->tb = bTB;
   g->cpp = bC;
   g->chunks = (D + bK - 1) / bK;
