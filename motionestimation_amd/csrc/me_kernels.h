@@ -48,6 +48,8 @@ struct QsadGeom {
   int wg_per_row;  // workgroups per block row
   int nbx_full;    // full-width blocks per row
   int aligned;     // 4-byte aligned global rows
+  int fold;        // SAD, S % 4 == 0: groups = S/2 cover dx in [-S, S-1]; the dx = +S
+                   // column is spread over lanes gi < K, one v_sad_u8 candidate each
 };
 
 hipError_t launch_search(const SearchArgs& p, hipStream_t stream, int* used_fast);

@@ -260,7 +260,8 @@ __device__ unsigned long long g_stamps[8 << 16];
 #define ME_STAMP(slot, v) do { } while (0)
 #endif
 
-// 32-bit lane keys (sad << 16 | j*4 + i) ordered like (cost, dy, dx); invalid
+// 32-bit lane keys (sad << 16 | j*8 + i) ordered like (cost, dy, dx); i = 4 is
+// the fold's dx = +S column (after every group dx of the same dy); invalid
 // candidates forced to sad 0xFFFF (> any valid SAD: B*B*255 <= 65280).
 // MASKJ = false on items whose whole dy range is valid (uniform per item).
 template <int K, bool MASKJ>
@@ -278,14 +279,44 @@ __device__ __forceinline__ uint32_t lane_best(const uint64_t (&acc)[K], uint32_t
       lo = jv ? lo : ~0u;
       hi = jv ? hi : ~0u;
     }
-    const uint32_t k0 = (lo << 16) | (uint32_t)(4 * j);
-    const uint32_t k1 = (lo & 0xFFFF0000u) | (uint32_t)(4 * j + 1);
-    const uint32_t k2 = (hi << 16) | (uint32_t)(4 * j + 2);
-    const uint32_t k3 = (hi & 0xFFFF0000u) | (uint32_t)(4 * j + 3);
+    const uint32_t k0 = (lo << 16) | (uint32_t)(8 * j);
+    const uint32_t k1 = (lo & 0xFFFF0000u) | (uint32_t)(8 * j + 1);
+    const uint32_t k2 = (hi << 16) | (uint32_t)(8 * j + 2);
+    const uint32_t k3 = (hi & 0xFFFF0000u) | (uint32_t)(8 * j + 3);
     b01 = min(b01, min(k0, k1));
     b23 = min(b23, min(k2, k3));
   }
   return min(b01, b23);
+}
+
+// Fold column: SAD of the lane's one dx = +S candidate (window rows row..row+H-1,
+// B bytes at byte offset `off` of the tile row, B-aligned) with v_sad_u8.
+template <int B, int H>
+__device__ __forceinline__ uint32_t tail_sad(const uint8_t* __restrict__ tile, int pitch,
+                                             uint32_t off, const uint32_t (&c)[B][B / 4]) {
+  const uint32_t lds0 = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) const uint8_t*)tile);
+  uint32_t o = lds0 + off;
+  uint32_t sad = 0;
+#pragma unroll
+  for (int y = 0; y < H; y++) {
+    if constexpr (B == 16) {
+      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+      typedef __attribute__((address_space(3))) const u32x4 lds_v4;
+      const u32x4 w = *reinterpret_cast<lds_v4*>((uintptr_t)o);
+      sad = __builtin_amdgcn_sad_u8(w[0], c[y][0], sad);
+      sad = __builtin_amdgcn_sad_u8(w[1], c[y][1], sad);
+      sad = __builtin_amdgcn_sad_u8(w[2], c[y][2], sad);
+      sad = __builtin_amdgcn_sad_u8(w[3], c[y][3], sad);
+    } else {
+      typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+      typedef __attribute__((address_space(3))) const u32x2 lds_v2;
+      const u32x2 w = *reinterpret_cast<lds_v2*>((uintptr_t)o);
+      sad = __builtin_amdgcn_sad_u8(w[0], c[y][0], sad);
+      sad = __builtin_amdgcn_sad_u8(w[1], c[y][1], sad);
+    }
+    o += pitch;
+  }
+  return sad;
 }
 
 // --------------------------------------------------------------- dot4 (SSD)
@@ -572,7 +603,12 @@ __global__ __launch_bounds__(1024) void me_fast_kernel(SearchArgs p, QsadGeom g)
     // task t -> (chunk, block, group) by multiply-high: t / G with the host's
     // verified magic, then / nb with a per-item magic (nb <= 16).
     const uint32_t magic_nb = 0xFFFFFFFFu / (uint32_t)it.nb + 1u;
-    for (int t = tid; t < T; t += nthr) {
+    // When T is not a multiple of the workgroup size the last round falls to
+    // the first waves; rotate which wave that is from item to item so no SIMD
+    // takes every extra round.
+    int vt = tid - 64 * ((bid + k) % (nthr >> 6));
+    if (vt < 0) vt += nthr;
+    for (int t = vt; t < T; t += nthr) {
       const int bg = (int)__umulhi((uint32_t)t, g.magic_groups);  // t / G
       const int gi = t - bg * G;
       const int lcr = it.nb == 1 ? bg : (int)__umulhi((uint32_t)bg, magic_nb);  // bg / nb
@@ -615,10 +651,17 @@ __global__ __launch_bounds__(1024) void me_fast_kernel(SearchArgs p, QsadGeom g)
       }
       const int w0 = (b * B) / 4 + gi;
       uint64_t acc[K];
-      if (it.h == B)
+      // fold: lane gi < K also owns candidate (dx = +S, dy index jt = gi)
+      const int jt = gi < K ? gi : K - 1;
+      const uint32_t toff = tile_off + (uint32_t)((lc * K + jt) * g.pitch + b * B + 2 * S);
+      uint32_t tsad = 0;
+      if (it.h == B) {
         qsad_lane<B, K, B>(smem, g.pitch, tile_off, lc * K, w0, c, acc);
-      else
+        if (g.fold) tsad = tail_sad<B, B>(smem, g.pitch, toff, c);
+      } else {
         qsad_lane<B, K, B / 2>(smem, g.pitch, tile_off, lc * K, w0, c, acc);
+        if (g.fold) tsad = tail_sad<B, B / 2>(smem, g.pitch, toff, c);
+      }
       // Waves with no frame-edge candidate (most of them) take the unmasked
       // epilogue: the test is wave-uniform, so there is no divergence.
       const int dxg = 4 * gi - S - it.a;  // dx of this lane's first candidate
@@ -643,13 +686,17 @@ __global__ __launch_bounds__(1024) void me_fast_kernel(SearchArgs p, QsadGeom g)
         }
         best = lane_best<K, true>(acc, mlo, mhi, jlo, jhi);
       }
+      if (g.fold) {
+        const bool tv = gi < K && jt >= jlo && jt <= jhi && S <= dxmax;
+        best = min(best, tv ? (tsad << 16) | (uint32_t)(8 * jt + 4) : ~0u);
+      }
 #if ME_ABLATE == 3  // diagnostic: no key atomics
       if (best == 0x12345u) {
 #else
       if (best < 0xFFFF0000u) {
 #endif
-        const int idx = (int)(best & 0xFFFFu);
-        const int dy = d0 + (idx >> 2) - S, dx = 4 * gi + (idx & 3) - S - it.a;
+        const int idx = (int)(best & 0xFFFFu), i = idx & 7;
+        const int dy = d0 + (idx >> 3) - S, dx = i == 4 ? S : 4 * gi + i - S - it.a;
         atomicMin(reinterpret_cast<unsigned long long*>(&keys[b]),
                   (unsigned long long)make_key(best >> 16, dx, dy));
       }
@@ -733,10 +780,12 @@ hipError_t launch_generic(const SearchArgs& p, int bx0, int nbx_range, int row0,
 }
 
 // Plan the fast kernels.  SAD lanes own 4 dx (one qsad group), SSD lanes one
-// dx; both own K dy.  Search (K, TB, chunks per pass) for the fewest idle
-// lanes at 256 threads per workgroup (4 workgroups of 4 waves per CU at the
-// kernels' <= 128 VGPRs), within the LDS budget; then prefer fewer passes and
-// smaller tiles (finer work items).
+// dx; both own K dy.  Search (fold, K, TB, chunks per pass) for the most
+// useful work per wave-task (dy padding, the masked 4th column of the last
+// SAD group or the fold's extra column, idle lanes of partly filled waves)
+// within the LDS budget; then prefer fewer passes and smaller tiles (finer
+// work items).  256 threads per workgroup: 4 workgroups of 4 waves per CU at
+// the kernels' <= 128 VGPRs.
 bool plan_fast(const SearchArgs& p, QsadGeom* g, int* k_out) {
   const int B = p.blk, S = p.range;
   if (B != 16 && B != 8) return false;
@@ -745,54 +794,89 @@ bool plan_fast(const SearchArgs& p, QsadGeom* g, int* k_out) {
   if (g->nbx_full < 1) return false;
   const bool sad = p.cost_kind == COST_SAD;
   const int D = 2 * S + 1;
-  g->groups = sad ? (2 * S + 3 + 1 + 3) / 4 : D;  // SAD: worst case a = 3
+  const int CW = B / 4;
+  // Fold needs a = 0 (S % 4 == 0) and the tail words of every block aligned
+  // for one ds_read of B bytes (b*B + 2S multiple of B: S % 8 == 0 for B = 16).
+  const bool fold_ok = sad && S % 4 == 0 && (B == 8 || S % 8 == 0);
   static const int Ks[] = {13, 11, 8};
-  // Tuning override (tools/plan_sweep.py only): ME_PLAN="K,tb,cpp,threads",
-  // 0 = free; read once per process.
-  static int force[4] = {-1, 0, 0, 0};
+  // Tuning override (tools/plan_sweep.py only): ME_PLAN="K,tb,cpp,threads[,fold]",
+  // 0 = free (fold: -1 = free); read once per process.
+  static int force[5] = {-1, 0, 0, 0, -1};
   if (force[0] < 0) {
     force[0] = 0;
     if (const char* e = getenv("ME_PLAN"))
-      sscanf(e, "%d,%d,%d,%d", &force[0], &force[1], &force[2], &force[3]);
+      sscanf(e, "%d,%d,%d,%d,%d", &force[0], &force[1], &force[2], &force[3], &force[4]);
   }
   const int thr = force[3] > 0 ? force[3] : 256;
   const int rows = p.block_row_end - p.block_row_begin;
   double best = -1;
-  int bK = 13, bTB = 1, bC = 1;
-  for (int K : Ks) {
-    if (force[0] && K != force[0]) continue;
-    const int chunks = (D + K - 1) / K;
-    const double kpad = (double)D / (chunks * K);
-    for (int tb = 1; tb <= 16; tb++) {
-      if (force[1] && tb != force[1]) continue;
-      // bytes the lanes touch per row (+ a <= 3, + alignment word)
-      const int width = (tb - 1) * B + (sad ? 4 * g->groups + B + 4 : 2 * S + 1 + 3 + B + 4);
-      int pt = (width + 15) & ~15;
-      if (((pt >> 4) & 1) == 0) pt += 16;
-      for (int cpp = chunks; cpp >= 1; cpp--) {
-        if (force[2] && cpp != force[2]) continue;
-        const long lds = 128 + 2 * ((long)tb * B * B + (long)(cpp * K + B - 1) * pt);
-        if (lds > QSAD_LDS_BUDGET) continue;
-        long slots = 0, work = 0;
-        int passes = 0;
-        for (int c0 = 0; c0 < chunks; c0 += cpp, passes++) {
-          const int t = tb * g->groups * (chunks - c0 < cpp ? chunks - c0 : cpp);
-          slots += (long)((t + thr - 1) / thr) * thr;
-          work += t;
-        }
-        // too few work items leave workgroup slots idle (and nothing to
-        // prefetch): aim for >= 2 items per resident workgroup (4 per CU).
-        const long items = (long)((g->nbx_full + tb - 1) / tb) * rows * passes;
-        const double fill = items >= 2048 ? 1.0 : (double)items / 2048;
-        const double score = kpad * work / slots * (0.7 + 0.3 * fill) - 0.004 * passes - 0.002 * tb;
-        if (score > best + 1e-9) {
-          best = score; bK = K; bTB = tb; bC = cpp;
-          g->pitch = pt;
+  int bK = 13, bTB = 1, bC = 1, bF = 0, bG = 1;
+  for (int fold = 0; fold <= 1; fold++) {
+    if (fold && !fold_ok) continue;
+    if (force[4] >= 0 && fold != force[4]) continue;
+    // SAD: worst case a = 3 without fold
+    const int G = sad ? (fold ? S / 2 : (2 * S + 3 + 1 + 3) / 4) : D;
+    // useful share of a lane's candidates (the last group's padding), and the
+    // fold's extra cost per task (one B-row v_sad_u8 column + its key)
+    const double use_dx = sad ? (fold ? 1.0 : (double)D / (4.0 * G)) : 1.0;
+    for (int K : Ks) {
+      if (force[0] && K != force[0]) continue;
+      if (fold && G < K) continue;
+      const int chunks = (D + K - 1) / K;
+      const double kpad = (double)D / (chunks * K);
+      const double tail = fold ? 0.5 * (B * CW + 16) / (K * B * CW * 4 + 340) : 0.0;
+      // Waves that hold whole (block, chunk) groups (64 % G == 0 or G % 64
+      // == 0) read one cur block and share one row range per wave: measured
+      // ~5 % faster than waves straddling blocks (8K B8: G 64 vs 65).
+      const double wave_align = (64 % G == 0 || G % 64 == 0) ? 1.03 : 1.0;
+      for (int tb = 1; tb <= 16; tb++) {
+        if (force[1] && tb != force[1]) continue;
+        // bytes the lanes touch per row (+ a <= 3, + alignment word)
+        const int width = (tb - 1) * B + (sad ? 4 * G + B + 4 : 2 * S + 1 + 3 + B + 4);
+        int pt = (width + 15) & ~15;
+        if (((pt >> 4) & 1) == 0) pt += 16;
+        for (int cpp = chunks; cpp >= 1; cpp--) {
+          if (force[2] && cpp != force[2]) continue;
+          const long lds = 128 + 2 * ((long)tb * B * B + (long)(cpp * K + B - 1) * pt);
+          if (lds > QSAD_LDS_BUDGET) continue;
+          int passes = 0;
+          for (int c0 = 0; c0 < chunks; c0 += cpp) passes++;
+          const long items = (long)((g->nbx_full + tb - 1) / tb) * rows * passes;
+          // Cost of an item in wave-tasks: its waves (a partly filled wave
+          // costs a whole one) + ~0.45 for staging, barrier and output
+          // (fitted on tools/plan_sweep.py runs).  With few items per
+          // workgroup (< 8 of 1024) a partial last round of the workgroup
+          // is not amortised: count whole rounds of `thr` lanes instead.
+          const bool many = items >= 8L * 1024;
+          double cost = 0, useful = 0;
+          for (int c0 = 0; c0 < chunks; c0 += cpp) {
+            const int t = tb * G * (chunks - c0 < cpp ? chunks - c0 : cpp);
+            const int rounds = (t + thr - 1) / thr;
+            // few items: every extra round lengthens the kernel's tail too
+            cost += (many ? (t + 63) / 64 : rounds * (thr / 64) + 0.5 * (rounds - 1)) + 0.45;
+            useful += t / 64.0;
+          }
+          // too few work items leave workgroup slots idle (and nothing to
+          // prefetch): aim for >= 2 items per resident workgroup (4 per CU).
+          const double fill = items >= 2048 ? 1.0 : (double)items / 2048;
+          // K = 13 measured best wherever it fits (more candidates per row load
+          // and per epilogue than the padding it costs).
+          const double kpref = K == 13 ? 1.0 : 0.95;
+          // the last tile of a block row holds nbx_full % tb blocks
+          const double tile_fill =
+              (double)g->nbx_full / ((double)((g->nbx_full + tb - 1) / tb) * tb);
+          const double score = kpad * kpref * wave_align * tile_fill * use_dx / (1.0 + tail) * useful / cost *
+                               (0.7 + 0.3 * fill) - 0.002 * tb;
+          if (score > best + 1e-9) {
+            best = score; bK = K; bTB = tb; bC = cpp; bF = fold; bG = G;
+          }
         }
       }
     }
   }
   if (best < 0) return false;  // nothing fits (only with an ME_PLAN override)
+  g->fold = bF;
+  g->groups = bG;
   g->tb = bTB;
   g->cpp = bC;
   g->chunks = (D + bK - 1) / bK;

@@ -22,10 +22,15 @@ def main():
     ap.add_argument("--tb", default="1,2,3,4,5,6")
     ap.add_argument("--cpp", default="0")
     ap.add_argument("--threads", default="256")
+    ap.add_argument("--fold", default="-1")
+    ap.add_argument("--plans", default="", help="explicit 'K,tb,cpp,thr,fold;...' (overrides the grid)")
     ap.add_argument("--iters", type=int, default=30)
     a = ap.parse_args()
-    plans = ["auto"] + [f"{k},{t},{c},{n}" for k, t, c, n in itertools.product(
-        a.K.split(","), a.tb.split(","), a.cpp.split(","), a.threads.split(","))]
+    plans = ["auto"] + [f"{k},{t},{c},{n},{f}" for k, t, c, n, f in itertools.product(
+        a.K.split(","), a.tb.split(","), a.cpp.split(","), a.threads.split(","),
+        a.fold.split(","))]
+    if a.plans:
+        plans = ["auto"] + a.plans.split(";")
     for plan in plans:
         env = dict(os.environ)
         if plan != "auto":
