@@ -260,8 +260,10 @@ __device__ unsigned long long g_stamps[8 << 16];
 #define ME_STAMP(slot, v) do { } while (0)
 #endif
 
-// 32-bit lane keys (sad << 16 | j*8 + i) ordered like (cost, dy, dx); i = 4 is
-// the fold's dx = +S column (after every group dx of the same dy); invalid
+// 32-bit lane keys (sad << 16 | j*5 + i) ordered like (cost, dy, dx); i = 4 is
+// the fold's dx = +S column (after every group dx of the same dy).  j*5 + i <=
+// 64 for K <= 13 keeps every index an inline constant (VOP3 on gfx950 takes
+// no literals: larger ones would each pin a VGPR and spill); invalid
 // candidates forced to sad 0xFFFF (> any valid SAD: B*B*255 <= 65280).
 // MASKJ = false on items whose whole dy range is valid (uniform per item).
 template <int K, bool MASKJ>
@@ -279,10 +281,10 @@ __device__ __forceinline__ uint32_t lane_best(const uint64_t (&acc)[K], uint32_t
       lo = jv ? lo : ~0u;
       hi = jv ? hi : ~0u;
     }
-    const uint32_t k0 = (lo << 16) | (uint32_t)(8 * j);
-    const uint32_t k1 = (lo & 0xFFFF0000u) | (uint32_t)(8 * j + 1);
-    const uint32_t k2 = (hi << 16) | (uint32_t)(8 * j + 2);
-    const uint32_t k3 = (hi & 0xFFFF0000u) | (uint32_t)(8 * j + 3);
+    const uint32_t k0 = (lo << 16) | (uint32_t)(5 * j);
+    const uint32_t k1 = (lo & 0xFFFF0000u) | (uint32_t)(5 * j + 1);
+    const uint32_t k2 = (hi << 16) | (uint32_t)(5 * j + 2);
+    const uint32_t k3 = (hi & 0xFFFF0000u) | (uint32_t)(5 * j + 3);
     b01 = min(b01, min(k0, k1));
     b23 = min(b23, min(k2, k3));
   }
@@ -408,10 +410,20 @@ __device__ __forceinline__ uint32_t lane_best_ssd(const uint32_t (&v)[K], int jl
 // maps such a destination byte offset to the buffer offset (any uint32: the
 // descriptor's range check returns zeros for offsets past the resident rows,
 // including negative ones, which wrap).
+// Lane index recomputed per call: an opaque copy of threadIdx.x keeps the
+// compiler from hoisting lane-derived staging addresses out of the item loop,
+// where they would stay live across the 128-VGPR task loop and spill.
+__device__ __forceinline__ int fresh_tid() {
+  int t = (int)threadIdx.x;
+  asm volatile("" : "+v"(t));
+  return t;
+}
+
 template <typename F>
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, uint8_t* lds_dst, int bytes,
                                       F src_off) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int tid = fresh_tid();
+  const int lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
   for (int s0 = wave * 1024; s0 < bytes; s0 += nw * 1024) {
     const int d = s0 + 16 * lane;
     // lanes past the end must not execute: an out-of-range lane would still
@@ -430,7 +442,8 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, uint8_t* lds_ds
 template <typename F>
 __device__ __forceinline__ void dma4(__amdgpu_buffer_rsrc_t rs, uint8_t* lds_dst, int bytes,
                                      F src_off) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int tid = fresh_tid();
+  const int lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
   for (int s0 = wave * 256; s0 < bytes; s0 += nw * 256) {
     const int d = s0 + 4 * lane;
     if (d < bytes)
@@ -472,7 +485,7 @@ __device__ __forceinline__ void stage_item(const SearchArgs& p, const QsadGeom& 
   uint8_t* tile = buf;
   uint8_t* cur = buf + g.tile_bytes;
   const int pitch = g.pitch, stride = p.stride;
-  const int tid = threadIdx.x, nthr = blockDim.x;
+  const int tid = fresh_tid(), nthr = blockDim.x;
   if (g.aligned) {
     // tile byte (r, x) <- ref(prow0 + r, X0 + x); zeros outside the resident rows.
     const int base = (it.prow0 - p.ref_row0) * stride + it.X0;
@@ -606,7 +619,7 @@ __global__ __launch_bounds__(1024) void me_fast_kernel(SearchArgs p, QsadGeom g)
     // When T is not a multiple of the workgroup size the last round falls to
     // the first waves; rotate which wave that is from item to item so no SIMD
     // takes every extra round.
-    int vt = tid - 64 * ((bid + k) % (nthr >> 6));
+    int vt = fresh_tid() - 64 * ((bid + k) % (nthr >> 6));
     if (vt < 0) vt += nthr;
     for (int t = vt; t < T; t += nthr) {
       const int bg = (int)__umulhi((uint32_t)t, g.magic_groups);  // t / G
@@ -688,15 +701,15 @@ __global__ __launch_bounds__(1024) void me_fast_kernel(SearchArgs p, QsadGeom g)
       }
       if (g.fold) {
         const bool tv = gi < K && jt >= jlo && jt <= jhi && S <= dxmax;
-        best = min(best, tv ? (tsad << 16) | (uint32_t)(8 * jt + 4) : ~0u);
+        best = min(best, tv ? (tsad << 16) | (uint32_t)(5 * jt + 4) : ~0u);
       }
 #if ME_ABLATE == 3  // diagnostic: no key atomics
       if (best == 0x12345u) {
 #else
       if (best < 0xFFFF0000u) {
 #endif
-        const int idx = (int)(best & 0xFFFFu), i = idx & 7;
-        const int dy = d0 + (idx >> 3) - S, dx = i == 4 ? S : 4 * gi + i - S - it.a;
+        const int idx = (int)(best & 0xFFFFu), jj = idx / 5, i = idx - 5 * jj;
+        const int dy = d0 + jj - S, dx = i == 4 ? S : 4 * gi + i - S - it.a;
         atomicMin(reinterpret_cast<unsigned long long*>(&keys[b]),
                   (unsigned long long)make_key(best >> 16, dx, dy));
       }
@@ -705,7 +718,9 @@ __global__ __launch_bounds__(1024) void me_fast_kernel(SearchArgs p, QsadGeom g)
       __syncthreads();  // every task of the tile has folded its key
       if (tid < it.nb) {
         const uint64_t kk = keys[tid];
-        keys[tid] = ~0ull;  // ready for this workgroup's next tile
+        uint64_t none = ~0ull;  // materialised here, not kept live (it spilled)
+        asm volatile("" : "+v"(none));
+        keys[tid] = none;  // ready for this workgroup's next tile
         const int out = (it.by - p.block_row_begin) * p.nbx + it.bx0 + tid;
         p.mv[2 * out] = (int16_t)((int)(kk & 0xFFFF) - 32768);
         p.mv[2 * out + 1] = (int16_t)((int)((kk >> 16) & 0xFFFF) - 32768);

@@ -9,7 +9,7 @@
 set -o pipefail
 TAG=${1:-r01}
 shift
-ARGS=${@:---steps 20 --warmup 3 --no-cpu}
+ARGS=${@:---steps 20 --warmup 3 --no-cpu --no-stream}
 OUT=gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
