@@ -82,6 +82,52 @@ static uint32_t cost_int(const uint8_t* ref, const uint8_t* cur, int stride,
   return s;
 }
 
+/* ssim.c:3-62 restated on u8 planes: means as float sums of ints (exact) over
+ * w*h; variances as float sums of (float(p) - mean)^2 in raster order; the
+ * cross term with the means truncated to int (computeCrossVar takes int
+ * means) accumulated in float from int products (exact: |sum| < 2^24); the
+ * standard deviations through double sqrt; then the three factors in float,
+ * left to right, no contraction (build with -ffp-contract=off). */
+static void ssim_stats(const uint8_t* p, int stride, int x0, int y0, int w, int h, float* mean,
+                       float* var) {
+  const int n = w * h;
+  float s = 0;
+  for (int oy = 0; oy < h; oy++)
+    for (int ox = 0; ox < w; ox++) s += (int)p[(size_t)(y0 + oy) * stride + x0 + ox];
+  const float m = s / n;
+  float v = 0;
+  for (int oy = 0; oy < h; oy++)
+    for (int ox = 0; ox < w; ox++) {
+      const int q = p[(size_t)(y0 + oy) * stride + x0 + ox];
+      v += (q - m) * (q - m);
+    }
+  *mean = m;
+  *var = v / n;
+}
+
+static float ssim_score(const uint8_t* ref, const uint8_t* cur, int stride, const orc_block* b,
+                        int cx, int cy) {
+  const int w = b->width, h = b->height, n = w * h;
+  const float C1 = 0.01f, C2 = 0.09f, C3 = 0.045f;  /* ssim.c:48, float from double */
+  float mr, vr, mp, vp;
+  ssim_stats(ref, stride, cx, cy, w, h, &mr, &vr);
+  ssim_stats(cur, stride, b->top_left_x, b->top_left_y, w, h, &mp, &vp);
+  const float sr = (float)sqrt((double)vr), sp = (float)sqrt((double)vp);
+  const int imr = (int)mr, imp = (int)mp;
+  float cv = 0;
+  for (int oy = 0; oy < h; oy++)
+    for (int ox = 0; ox < w; ox++) {
+      const int r = ref[(size_t)(cy + oy) * stride + cx + ox];
+      const int c = cur[(size_t)(b->top_left_y + oy) * stride + b->top_left_x + ox];
+      cv += (r - imr) * (c - imp);
+    }
+  cv = cv / n;
+  const float lum = (2 * mr * mp + C1) / (mr * mr + mp * mp + C1);
+  const float con = (2 * sr * sp + C2) / (sr * sr + sp * sp + C2);
+  const float str = (cv + C3) / (sr * sp + C3);
+  return lum * con * str;
+}
+
 /* main.c:39-64 + 67-82: y outer, x inner, keep the first strict minimum. */
 uint32_t orc_search_block(const uint8_t* ref, const uint8_t* cur, int width,
                           int height, int stride, const orc_block* b,
@@ -105,6 +151,24 @@ uint32_t orc_search_block(const uint8_t* ref, const uint8_t* cur, int width,
     *mvy = best_y;
     return cost_int(ref, cur, stride, b, b->top_left_x + best_x,
                     b->top_left_y + best_y, ORC_SSD);
+  }
+  if (kind == ORC_SSIM) {  /* ssim.c:83-108: maximise, strict > from 0 */
+    float best = 0;
+    for (int y = wy0; y <= wy1 - b->height + 1; y++)
+      for (int x = wx0; x <= wx1 - b->width + 1; x++) {
+        const float sc = ssim_score(ref, cur, stride, b, x, y);
+        if (sc > best) {
+          best = sc;
+          best_x = x - b->top_left_x;
+          best_y = y - b->top_left_y;
+        }
+      }
+    if (mse) *mse = best;
+    *mvx = best_x;
+    *mvy = best_y;
+    uint32_t bits;
+    memcpy(&bits, &best, 4);
+    return bits;
   }
   uint32_t best = 0xFFFFFFFFu;
   int found = 0;

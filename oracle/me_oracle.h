@@ -13,6 +13,8 @@
  *   frame-clamped window    src/cpu/main.c:67-82
  *   per-block dispatch      src/cpu/main.c:141-158 (thread pool, one job per block)
  *   MC / diff / PSNR        src/common/utils.c:94-164
+ *   SSIM cost (maximised)   src/common/ssim.c:3-62 (score), :83-108 (raster
+ *                           search, strict > from 0), src/cpu/main_ssim.c:15-29
  * Pinned against the real reference: tests/golden/ holds MV fields dumped by
  * oracle/_ref/ref_dump (the unmodified reference objects), and the published
  * results/cpu/foreman/output_4_{7,15}.yuv planes.
@@ -27,8 +29,13 @@ extern "C" {
 
 /* Cost kinds.  ORC_MSE_FLOAT replays the reference arithmetic literally
  * (float accumulation, float divide); ORC_SSD / ORC_SAD use exact integer
- * accumulation with the same loop order and tie rule. */
-enum { ORC_SSD = 0, ORC_SAD = 1, ORC_MSE_FLOAT = 2 };
+ * accumulation with the same loop order and tie rule.  ORC_SSIM replays
+ * src/common/ssim.c: the first candidate in raster order whose float score
+ * is strictly greater than every earlier one and than 0; the returned "cost"
+ * is the score's float bits, *mse the score.  If no candidate scores above 0
+ * the reference leaves its MV uninitialised (ssim.c:87-104); here it is
+ * (0, 0) with score 0. */
+enum { ORC_SSD = 0, ORC_SAD = 1, ORC_MSE_FLOAT = 2, ORC_SSIM = 3 };
 
 typedef struct orc_block {
   int idx_x, idx_y;

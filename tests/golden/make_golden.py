@@ -5,7 +5,9 @@ Run in the build container (where /root/reference exists) after
 ``make -C oracle ref``.  For every case it runs ``oracle/_ref/ref_dump`` -- a
 driver linked against the unmodified reference objects that calls
 ``findBestBlkMse`` (src/cpu/main.c:67) per block -- and stores one 12-byte
-record per block: int32 mvx, int32 mvy, float32 mse.
+record per block: int32 mvx, int32 mvy, float32 mse.  SSIM cases come from
+``oracle/_ref/ref_dump_ssim`` (``findBestBlkSSIM``, src/cpu/main_ssim.c:15);
+``--ssim`` regenerates only those.
 
 Inputs:
   * frames/ForemanYF{1,2,4}.yuv   copied verbatim from /root/reference/frames
@@ -34,6 +36,7 @@ from motionestimation_amd import synth  # noqa: E402
 
 REF = os.environ.get("ME_REFERENCE", "/root/reference")
 REF_DUMP = os.path.join(REPO, "oracle", "_ref", "ref_dump")
+REF_DUMP_SSIM = os.path.join(REPO, "oracle", "_ref", "ref_dump_ssim")
 FRAMES = os.path.join(HERE, "frames")
 MV = os.path.join(HERE, "mv")
 PUB = os.path.join(HERE, "published")
@@ -100,12 +103,72 @@ SYNTH_CASES = [
 ]
 
 
-def run_ref(cur_path, ref_path, w, h, blk, span, out):
-    subprocess.run([REF_DUMP, cur_path, ref_path, str(w), str(h), str(blk), str(span), out],
-                   check=True)
+# SSIM goldens (src/common/ssim.c via oracle/_ref/ref_dump_ssim): record =
+# int32 mvx, int32 mvy, float32 ssim.  Blocks whose best score is not > 0 keep
+# the reference's uninitialised MV (ssim.c:87-104): compare their scores only.
+SSIM_FOREMAN = [
+    ("ssim_foreman21_b16_s7", "ForemanYF2", "ForemanYF1", 16, 7),
+    ("ssim_foreman21_b16_s16", "ForemanYF2", "ForemanYF1", 16, 16),
+    ("ssim_foreman41_b8_s4", "ForemanYF4", "ForemanYF1", 8, 4),    # 19 blocks without a score > 0
+    ("ssim_foreman14_b16_s12", "ForemanYF1", "ForemanYF4", 16, 12),
+]
+SSIM_SMALL = [
+    ("noise_100x75", 16, 9), ("flat_64x48", 16, 7), ("translate_128x96", 8, 8),
+    ("tiny_7x5", 16, 4), ("contrast_96x96", 32, 6), ("stripes_80x60", 8, 6),
+]
+SSIM_SYNTH = [("ssim_synth1080p_b16_s32", "1080p", 16, 32)]
+
+
+def run_ref(cur_path, ref_path, w, h, blk, span, out, tool=None):
+    subprocess.run([tool or REF_DUMP, cur_path, ref_path, str(w), str(h), str(blk), str(span),
+                    out], check=True)
+
+
+def ssim_cases(manifest) -> None:
+    """(Re)generate manifest["ssim_cases"] only; frames must already be there."""
+    if not os.path.exists(REF_DUMP_SSIM):
+        sys.exit("build oracle/_ref first: make -C oracle ref")
+    manifest["ssim_cases"] = []
+    manifest["ssim_format"] = ("per block int32 mvx, int32 mvy, float32 ssim (LE); MV undefined "
+                               "in the reference where ssim <= 0")
+
+    def add(name, cur_key, ref_key, cur_path, ref_path, w, h, blk, span):
+        out = os.path.join(MV, name + ".bin")
+        run_ref(cur_path, ref_path, w, h, blk, span, out, REF_DUMP_SSIM)
+        manifest["ssim_cases"].append({"name": name, "cur": cur_key, "ref": ref_key, "width": w,
+                                       "height": h, "blk": blk, "span": span, "cost": "ssim",
+                                       "mv": f"mv/{name}.bin",
+                                       "sha256": sha(open(out, "rb").read())})
+        print("golden", name, flush=True)
+
+    for name, c, r, blk, span in SSIM_FOREMAN:
+        add(name, c, r, os.path.join(FRAMES, c + ".yuv"), os.path.join(FRAMES, r + ".yuv"),
+            352, 288, blk, span)
+    for fname, blk, span in SSIM_SMALL:
+        info = manifest["frames"][f"syn_{fname}_ref"]
+        add(f"ssim_syn_{fname}_b{blk}_s{span}", f"syn_{fname}_cur", f"syn_{fname}_ref",
+            os.path.join(FRAMES, f"syn_{fname}_cur.yuv"), os.path.join(FRAMES, f"syn_{fname}_ref.yuv"),
+            info["width"], info["height"], blk, span)
+    with tempfile.TemporaryDirectory() as td:
+        for name, cfg, blk, span in SSIM_SYNTH:
+            ref, cur = synth.named_pair(cfg)
+            h, w = ref.shape
+            rp, cp = os.path.join(td, "ref.yuv"), os.path.join(td, "cur.yuv")
+            ref.tofile(rp)
+            cur.tofile(cp)
+            add(name, f"synth:{cfg}:cur", f"synth:{cfg}:ref", cp, rp, w, h, blk, span)
 
 
 def main() -> None:
+    if "--ssim" in sys.argv:  # refresh the SSIM cases, keep everything else
+        path = os.path.join(HERE, "manifest.json")
+        with open(path) as f:
+            manifest = json.load(f)
+        ssim_cases(manifest)
+        with open(path, "w") as f:
+            json.dump(manifest, f, indent=1, sort_keys=True)
+            f.write("\n")
+        return
     if not os.path.exists(REF_DUMP):
         sys.exit("build oracle/_ref first: make -C oracle ref")
     for d in (FRAMES, MV, PUB):
@@ -165,6 +228,7 @@ def main() -> None:
             manifest["frames"][f"synth:{cfg}:cur"] = {"width": w, "height": h,
                                                       "sha256": sha(cur.tobytes())}
             add_case(name, f"synth:{cfg}:cur", f"synth:{cfg}:ref", cp, rp, w, h, blk, span)
+    ssim_cases(manifest)
 
     with open(os.path.join(HERE, "manifest.json"), "w") as f:
         json.dump(manifest, f, indent=1, sort_keys=True)

@@ -15,8 +15,8 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_DIR = os.path.join(REPO, "oracle")
 GOLDEN = os.path.join(REPO, "tests", "golden")
 
-SSD, SAD, MSE_FLOAT = 0, 1, 2
-_KIND = {"ssd": SSD, "sad": SAD, "mse": MSE_FLOAT}
+SSD, SAD, MSE_FLOAT, SSIM = 0, 1, 2, 3
+_KIND = {"ssd": SSD, "sad": SAD, "mse": MSE_FLOAT, "ssim": 3}
 
 _lib = None
 

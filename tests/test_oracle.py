@@ -18,7 +18,7 @@ def _cases(manifest, big=False):
 
 
 def test_golden_files_intact(manifest):
-    for c in manifest["cases"]:
+    for c in manifest["cases"] + manifest["ssim_cases"]:
         raw = open(os.path.join(O.GOLDEN, c["mv"]), "rb").read()
         assert hashlib.sha256(raw).hexdigest() == c["sha256"], c["name"]
     for key, info in manifest["frames"].items():
@@ -118,3 +118,19 @@ def test_sad_restatement_small_bruteforce():
                     if best is None or s < best[0]:
                         best = (s, x - tlx, y - tly)
             assert (cost[i], mv[i, 0], mv[i, 1]) == best
+
+
+def test_oracle_ssim_matches_reference_goldens(manifest):
+    """SSIM (src/common/ssim.c) restated: score bits identical to the unmodified
+    reference on every block; MVs identical wherever the best score is > 0
+    (elsewhere the reference's MV is uninitialised, ssim.c:87-104)."""
+    for c in manifest["ssim_cases"]:
+        cur, ref = O.load_frame(c["cur"], manifest), O.load_frame(c["ref"], manifest)
+        gmv, gscore = O.load_case(c)
+        mv, bits, score = O.full_search(ref, cur, c["blk"], c["span"], "ssim")
+        np.testing.assert_array_equal(score.view(np.uint32), gscore.view(np.uint32),
+                                      err_msg=c["name"])
+        np.testing.assert_array_equal(bits, gscore.view(np.uint32), err_msg=c["name"])
+        pos = gscore > 0
+        np.testing.assert_array_equal(mv[pos].astype(np.int32), gmv[pos], err_msg=c["name"])
+        assert (mv[~pos] == 0).all()  # defined as (0, 0) here
