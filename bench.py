@@ -51,7 +51,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--mode", choices=["frames", "stripe"], default="frames")
     ap.add_argument("--config", choices=list(CONFIGS), default="1080p")
-    ap.add_argument("--cost", choices=["sad", "ssd"], default="sad")
+    ap.add_argument("--cost", choices=["sad", "ssd", "ssim"], default="sad")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-stream", action="store_true",
                     help="skip the host frame-pair streaming leg (PCIe-inclusive, not `value`)")
@@ -61,23 +61,41 @@ def parse():
     return ap.parse_args()
 
 
+def _block_candidates(w, h, blk, span, bx, by):
+    """Exact candidates of one block under the reference's clamping (main.c:73-76)."""
+    tlx, tly = bx * blk, by * blk
+    bw, bh = min(blk, w - tlx), min(blk, h - tly)
+    nx = min(span, w - bw - tlx) - max(-span, -tlx) + 1
+    ny = min(span, h - bh - tly) - max(-span, -tly) + 1
+    return nx * ny
+
+
 def cpu_baselines(ref, cur, blk, span, cost, threads, cands):
     """Rank 0, N=1 only: the oracle restatement (port) timed on the host cores
     on the same frame pair, and the reference's own binary (oracle/_ref/mes,
     MSE cost, its hard-coded 100-thread pool) when it was built."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import oracle_lib as O
+    h, w = ref.shape
+    nbx, nby = (w + blk - 1) // blk, (h + blk - 1) // blk
+    begin, end, what = 0, nbx * nby, "the full"
+    if cost == "ssim":  # ~40x the work per candidate: a bounded sample of 4 middle block rows
+        r0 = max(0, nby // 2 - 2)
+        begin, end = r0 * nbx, min(nby, r0 + 4) * nbx
+        what = f"block rows {r0}..{min(nby, r0 + 4) - 1} of the"
+        cands = sum(_block_candidates(w, h, blk, span, i % nbx, i // nbx)
+                    for i in range(begin, end))
     times = []
     for _ in range(5):
         t0 = time.perf_counter()
-        O.full_search(ref, cur, blk, span, cost, threads=threads)
+        O.full_search(ref, cur, blk, span, cost, threads=threads, begin=begin, end=end)
         times.append(time.perf_counter() - t0)
     med = statistics.median(times)
     out = {"value": cands / med, "unit": "candidates/s", "cores": threads, "kind": "port",
-           "sample": f"the full {ref.shape[1]}x{ref.shape[0]} B{blk} +-{span} {cost.upper()} frame, "
+           "sample": f"{what} {w}x{h} B{blk} +-{span} {cost.upper()} frame, "
                      f"oracle/me_oracle.c -O2, {threads} pthreads, median of 5 ({med*1e3:.1f} ms)"}
     mes = os.path.join(REPO, "oracle", "_ref", "mes")
-    if os.path.exists(mes):
+    if os.path.exists(mes) and cost != "ssim":
         with tempfile.TemporaryDirectory() as td:
             rp, cp = os.path.join(td, "ref.yuv"), os.path.join(td, "cur.yuv")
             ref.tofile(rp)
@@ -283,6 +301,8 @@ def main():
                               "frac": absdiffs / (kern_ms / 1e3) / VALU_PEAK_ABSDIFF}},
         "cpu_baseline": None,
     }
+    if args.cost == "ssim":  # float chains, not abs-diffs: no VALU-peak claim
+        line["roofline"]["valu"] = None
     if parity is not None:
         line["stripe_gather_parity"] = parity
     if rank == 0 and world == 1 and not args.no_cpu:

@@ -30,6 +30,8 @@
  *     searched with the reference's float accumulation replayed exactly.
  *   - ME_COST_SAD: same loops and tie rule with |cur - ref| (the reference
  *     has no SAD; parity is against the repo's CPU restatement).
+ *   - ME_COST_SSIM: the reference's SSIM search (src/common/ssim.c:3-108,
+ *     src/cpu/main_ssim.c:15-29), float arithmetic replayed in its order.
  *
  * Conventions: host buffers are caller-owned; host entry points are
  * synchronous on return.  A context is used by one host thread at a time.
@@ -59,7 +61,10 @@ typedef enum {
 
 typedef enum {
   ME_COST_SSD = 0, /* reference parity: float MSE argmin; cost = SSD */
-  ME_COST_SAD = 1  /* sum of absolute differences */
+  ME_COST_SAD = 1, /* sum of absolute differences */
+  ME_COST_SSIM = 2 /* reference parity with src/common/ssim.c: float SSIM argmax
+                      (first strict maximum above 0); cost = the score's float
+                      bits; MV (0, 0) and cost 0 where no score is above 0 */
 } me_cost;
 
 /* Limits of this build. */

@@ -52,7 +52,8 @@ me_status check_args(me_ctx* c, const void* ref, const void* cur, int width, int
   if (stride < width) return fail(c, ME_EINVAL, "stride %d < width %d", stride, width);
   if (blk < 1 || blk > ME_MAX_BLOCK) return fail(c, ME_EINVAL, "block_size %d", blk);
   if (range < 0 || range > ME_MAX_RANGE) return fail(c, ME_EINVAL, "search_range %d", range);
-  if (cost != ME_COST_SSD && cost != ME_COST_SAD) return fail(c, ME_EINVAL, "cost %d", cost);
+  if (cost != ME_COST_SSD && cost != ME_COST_SAD && cost != ME_COST_SSIM)
+    return fail(c, ME_EINVAL, "cost %d", cost);
   return ME_OK;
 }
 

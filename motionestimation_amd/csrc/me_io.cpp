@@ -41,7 +41,7 @@ bool bad_geometry(int width, int height, me_yuv_layout layout) {
 bool valid_header(const me_mv_header& h) {
   return memcmp(h.magic, "MEMV", 4) == 0 && h.version == 1 && h.width > 0 && h.height > 0 &&
          h.block_size > 0 && h.block_size <= ME_MAX_BLOCK && h.search_range >= 0 &&
-         (h.cost == ME_COST_SSD || h.cost == ME_COST_SAD);
+         (h.cost == ME_COST_SSD || h.cost == ME_COST_SAD || h.cost == ME_COST_SSIM);
 }
 
 }  // namespace

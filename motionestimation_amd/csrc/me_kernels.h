@@ -6,7 +6,7 @@
 
 namespace me {
 
-enum { COST_SSD = 0, COST_SAD = 1 };
+enum { COST_SSD = 0, COST_SAD = 1, COST_SSIM = 2 };
 
 constexpr int GENERIC_THREADS = 256;
 constexpr int GENERIC_LDS_BUDGET = 60 * 1024;
@@ -56,6 +56,9 @@ hipError_t launch_search(const SearchArgs& p, hipStream_t stream, int* used_fast
 hipError_t launch_generic(const SearchArgs& p, int bx0, int nbx_range, int row0, int nrows,
                           hipStream_t stream);
 bool plan_fast(const SearchArgs& p, QsadGeom* g, int* k_out);
+
+// SSIM-cost search (me_ssim.hip): every block of rows [block_row_begin, block_row_end).
+hipError_t launch_ssim(const SearchArgs& p, hipStream_t stream);
 
 // Consumers of the MV field (me_post.hip).
 hipError_t launch_compensate(const uint8_t* ref, const uint8_t* cur, int width, int height,

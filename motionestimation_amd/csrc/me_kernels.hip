@@ -1019,9 +1019,10 @@ static bool cached_plan(const SearchArgs& p, QsadGeom* g, int* K) {
 hipError_t launch_search(const SearchArgs& p, hipStream_t stream, int* used_fast) {
   const int r0 = p.block_row_begin, r1 = p.block_row_end;
   if (r1 <= r0) return hipSuccess;
+  if (used_fast) *used_fast = 0;
+  if (p.cost_kind == COST_SSIM) return launch_ssim(p, stream);
   QsadGeom g;
   int K = 0;
-  if (used_fast) *used_fast = 0;
   if (!cached_plan(p, &g, &K)) return launch_generic(p, 0, p.nbx, r0, r1 - r0, stream);
   // The qsad body is instantiated for full-height blocks and for h = B/2 (the
   // 1080p bottom row); any other partial bottom row goes to the generic kernel.

@@ -1,0 +1,166 @@
+// me_ssim.hip -- SSIM-cost full search, bit-exact with the
+// reference's CPU SSIM search (souravBhat/MotionEstimation src/common/ssim.c:3-108,
+// src/cpu/main_ssim.c:15-29).
+//
+// The reference maximises a float SSIM score per candidate (first strict
+// maximum above 0 in raster order).  Every float operation is replayed in the
+// reference's order with round-to-nearest intrinsics (no contraction):
+//   mean   = (float) sum(p) / (float)(w*h)       sum of ints is exact in float
+//   var    = float chain sum((float)p - mean)^2 in raster order, / (w*h)
+//   cross  = float chain of int products (p - (int)mean_r)(c - (int)mean_c)
+//            (computeCrossVar takes int means), / (w*h)
+//   stddev = (float) sqrt((double) var)
+//   score  = lum * con * str, each factor as written in ssim.c:53-56
+// The argmax is a min over 64-bit keys (0x7FFFFFFF - bits(score)) << 32 |
+// (dy, dx): scores > 0 are ordered by their bits, ties go to the smallest
+// (dy, dx) -- the reference's first strict maximum.  Blocks with no score
+// above 0 get MV (0, 0) and cost 0 (the reference leaves them uninitialised).
+// block_cost carries the float bits of the best score.
+//
+// One workgroup per block, one candidate per lane per step; the block and
+// its window are staged in LDS when they fit.  Float-latency bound (two
+// dependent w*h chains per candidate), not a hot path of the headline metric.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "me_kernels.h"
+
+namespace me {
+
+namespace {
+
+constexpr int SSIM_THREADS = 256;
+
+__device__ __forceinline__ uint64_t wave_min(uint64_t v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint64_t o = __shfl_xor(v, off, 64);
+    v = o < v ? o : v;
+  }
+  return v;
+}
+
+// ssim.c:3-28 for one w x h patch at p (row pitch `pitch`): mean and variance.
+__device__ __forceinline__ void patch_stats(const uint8_t* p, int pitch, int w, int h, float nf,
+                                            float* mean, float* var) {
+  int s = 0;
+  for (int y = 0; y < h; y++)
+    for (int x = 0; x < w; x++) s += p[y * pitch + x];
+  const float m = __fdiv_rn((float)s, nf);
+  float v = 0.f;
+  for (int y = 0; y < h; y++)
+    for (int x = 0; x < w; x++) {
+      const float d = __fsub_rn((float)p[y * pitch + x], m);
+      v = __fadd_rn(v, __fmul_rn(d, d));
+    }
+  *mean = m;
+  *var = __fdiv_rn(v, nf);
+}
+
+__device__ __forceinline__ float sqrt_via_double(float v) {
+  return __double2float_rn(__dsqrt_rn((double)v));
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(SSIM_THREADS) void me_ssim_kernel(SearchArgs p, int row0,
+                                                               int win_lds_bytes) {
+  extern __shared__ __align__(16) uint8_t smem[];
+  __shared__ uint64_t red[SSIM_THREADS / 64];
+  const int tid = threadIdx.x;
+  const int bx = (int)(blockIdx.x % (unsigned)p.nbx);
+  const int by = row0 + (int)(blockIdx.x / (unsigned)p.nbx);
+  const int B = p.blk, S = p.range;
+  const int tlx = bx * B, tly = by * B;
+  const int w = min(B, p.width - tlx), h = min(B, p.height - tly);
+  const int wx0 = max(tlx - S, 0), wy0 = max(tly - S, 0);
+  const int wx1 = min(tlx + w - 1 + S, p.width - 1), wy1 = min(tly + h - 1 + S, p.height - 1);
+  const int ncx = wx1 - w + 1 - wx0 + 1, ncy = wy1 - h + 1 - wy0 + 1;
+  const int ww = wx1 - wx0 + 1, wh = wy1 - wy0 + 1;
+
+  uint8_t* cblk = smem;                        // w*h bytes, pitch w
+  uint8_t* win = smem + ((B * B + 15) & ~15);  // ww*wh bytes when staged
+  const bool staged = win_lds_bytes >= ww * wh;
+  for (int i = tid; i < w * h; i += SSIM_THREADS) {
+    const int oy = i / w, ox = i - oy * w;
+    cblk[i] = p.cur[(ptrdiff_t)(tly + oy - p.cur_row0) * p.stride + tlx + ox];
+  }
+  if (staged)
+    for (int i = tid; i < ww * wh; i += SSIM_THREADS) {
+      const int oy = i / ww, ox = i - oy * ww;
+      win[i] = p.ref[(ptrdiff_t)(wy0 + oy - p.ref_row0) * p.stride + wx0 + ox];
+    }
+  __syncthreads();
+
+  const float nf = (float)(w * h);
+  const float C1 = 0.01f, C2 = 0.09f, C3 = 0.045f;  // ssim.c:48
+  // Statistics of the current block (the reference recomputes them for every
+  // candidate; they are the same numbers).
+  float mp, vp;
+  patch_stats(cblk, w, w, h, nf, &mp, &vp);
+  const float sp = sqrt_via_double(vp);
+  const int imp = (int)mp;  // truncation, as the int parameter of computeCrossVar
+
+  uint64_t best = ~0ull;
+  const int ncand = ncx * ncy;
+  for (int t = tid; t < ncand; t += SSIM_THREADS) {
+    const int cy = t / ncx, cx = t - cy * ncx;
+    const uint8_t* r = staged ? win + cy * ww + cx
+                              : p.ref + (ptrdiff_t)(wy0 + cy - p.ref_row0) * p.stride + wx0 + cx;
+    const int rp = staged ? ww : p.stride;
+    float mr, vr;
+    patch_stats(r, rp, w, h, nf, &mr, &vr);
+    const float sr = sqrt_via_double(vr);
+    const int imr = (int)mr;
+    float cv = 0.f;
+    for (int y = 0; y < h; y++)
+      for (int x = 0; x < w; x++)
+        cv = __fadd_rn(cv, (float)((r[y * rp + x] - imr) * (cblk[y * w + x] - imp)));
+    cv = __fdiv_rn(cv, nf);
+    const float lum = __fdiv_rn(__fadd_rn(__fmul_rn(__fmul_rn(2.f, mr), mp), C1),
+                                __fadd_rn(__fadd_rn(__fmul_rn(mr, mr), __fmul_rn(mp, mp)), C1));
+    const float con = __fdiv_rn(__fadd_rn(__fmul_rn(__fmul_rn(2.f, sr), sp), C2),
+                                __fadd_rn(__fadd_rn(__fmul_rn(sr, sr), __fmul_rn(sp, sp)), C2));
+    const float str = __fdiv_rn(__fadd_rn(cv, C3), __fadd_rn(__fmul_rn(sr, sp), C3));
+    const float score = __fmul_rn(__fmul_rn(lum, con), str);
+    if (score > 0.f) {
+      const int dx = wx0 + cx - tlx, dy = wy0 + cy - tly;
+      const uint64_t key = ((uint64_t)(0x7FFFFFFFu - __float_as_uint(score)) << 32) |
+                           ((uint32_t)(dy + 32768) << 16) | (uint32_t)(dx + 32768);
+      best = key < best ? key : best;
+    }
+  }
+  best = wave_min(best);
+  if ((tid & 63) == 0) red[tid >> 6] = best;
+  __syncthreads();
+  if (tid == 0) {
+    uint64_t b = red[0];
+#pragma unroll
+    for (int i = 1; i < SSIM_THREADS / 64; i++) b = red[i] < b ? red[i] : b;
+    int dx = 0, dy = 0;
+    uint32_t bits = 0;
+    if (b != ~0ull) {
+      dx = (int)(b & 0xFFFF) - 32768;
+      dy = (int)((b >> 16) & 0xFFFF) - 32768;
+      bits = 0x7FFFFFFFu - (uint32_t)(b >> 32);
+    }
+    const int out = (by - p.block_row_begin) * p.nbx + bx;
+    p.mv[2 * out] = (int16_t)dx;
+    p.mv[2 * out + 1] = (int16_t)dy;
+    if (p.cost) p.cost[out] = bits;
+  }
+}
+
+hipError_t launch_ssim(const SearchArgs& p, hipStream_t stream) {
+  const int rows = p.block_row_end - p.block_row_begin;
+  if (rows <= 0 || p.nbx <= 0) return hipSuccess;
+  const int B = p.blk;
+  long win = (long)(B + 2 * p.range) * (B + 2 * p.range);
+  const int cur = (B * B + 15) & ~15;
+  if (cur + win > GENERIC_LDS_BUDGET) win = 0;  // read the window from global memory
+  hipLaunchKernelGGL(me_ssim_kernel, dim3((unsigned)(rows * p.nbx)), dim3(SSIM_THREADS),
+                     cur + (int)win, stream, p, p.block_row_begin, (int)win);
+  return hipGetLastError();
+}
+
+}  // namespace me

@@ -13,10 +13,10 @@ import ctypes
 import numpy as np
 
 from . import _lib
-from ._lib import ME_COST_SAD, ME_COST_SSD, MEError, check
+from ._lib import ME_COST_SAD, ME_COST_SSD, ME_COST_SSIM, MEError, check
 
-_COST = {"ssd": ME_COST_SSD, "mse": ME_COST_SSD, "sad": ME_COST_SAD,
-         ME_COST_SSD: ME_COST_SSD, ME_COST_SAD: ME_COST_SAD}
+_COST = {"ssd": ME_COST_SSD, "mse": ME_COST_SSD, "sad": ME_COST_SAD, "ssim": ME_COST_SSIM,
+         ME_COST_SSD: ME_COST_SSD, ME_COST_SAD: ME_COST_SAD, ME_COST_SSIM: ME_COST_SSIM}
 
 
 def cost_code(cost) -> int:

@@ -117,6 +117,11 @@ SSIM_SMALL = [
     ("tiny_7x5", 16, 4), ("contrast_96x96", 32, 6), ("stripes_80x60", 8, 6),
 ]
 SSIM_SYNTH = [("ssim_synth1080p_b16_s32", "1080p", 16, 32)]
+# The reference SSIM driver end to end (oracle/_ref/mes_ssim = src/cpu/main_ssim.c):
+# its score line and the sha256 of its 5-plane output (cases where every block
+# has a score > 0, so its MC plane is defined).
+SSIM_DRIVER = [("ForemanYF2", "ForemanYF1", 16, 7), ("ForemanYF1", "ForemanYF4", 16, 12)]
+MES_SSIM = os.path.join(REPO, "oracle", "_ref", "mes_ssim")
 
 
 def run_ref(cur_path, ref_path, w, h, blk, span, out, tool=None):
@@ -149,6 +154,17 @@ def ssim_cases(manifest) -> None:
         add(f"ssim_syn_{fname}_b{blk}_s{span}", f"syn_{fname}_cur", f"syn_{fname}_ref",
             os.path.join(FRAMES, f"syn_{fname}_cur.yuv"), os.path.join(FRAMES, f"syn_{fname}_ref.yuv"),
             info["width"], info["height"], blk, span)
+    manifest["ssim_driver"] = []
+    with tempfile.TemporaryDirectory() as td:
+        for cur, ref, blk, span in SSIM_DRIVER:
+            r = subprocess.run([MES_SSIM, os.path.join(FRAMES, cur + ".yuv"),
+                                os.path.join(FRAMES, ref + ".yuv"), td, str(blk), str(span),
+                                "352", "288"], check=True, capture_output=True, text=True)
+            line = [l for l in r.stdout.splitlines() if l.startswith("Original Score")][0]
+            out = open(os.path.join(td, f"output_{blk}_{span}.yuv"), "rb").read()
+            manifest["ssim_driver"].append({"cur": cur, "ref": ref, "blk": blk, "span": span,
+                                            "score_line": line, "output_sha256": sha(out)})
+            print("driver", cur, ref, blk, span, line, flush=True)
     with tempfile.TemporaryDirectory() as td:
         for name, cfg, blk, span in SSIM_SYNTH:
             ref, cur = synth.named_pair(cfg)

@@ -6,7 +6,9 @@
  * with the thread-pool dispatch (main.c:144-158) replaced by one
  * me_full_search() call through include/me.h, and the post-processing
  * (main.c:160-178) by me_compensate_planes().  Extra trailing options:
- *   --cost ssd|sad      (default ssd = the reference's MSE choice)
+ *   --cost ssd|sad|ssim (default ssd = the reference's MSE choice; ssim = the
+ *                       reference's SSIM driver src/cpu/main_ssim.c, whose
+ *                       stdout -- score lines instead of PSNR -- is mirrored)
  *   --gpus N            stripe the search over devices 0..N-1 (RCCL gather)
  *   --mv FILE           MV field + costs as a MEMV file (include/me.h, me_mv_write)
  * Errors print a message and return 1 (no exit() inside the library).
@@ -46,7 +48,8 @@ int main(int argc, char** argv) {
   const char* mv_path = NULL;
   for (int i = 1; i < argc; i++) {
     if (!strcmp(argv[i], "--cost") && i + 1 < argc) {
-      cost = !strcmp(argv[++i], "sad") ? ME_COST_SAD : ME_COST_SSD;
+      ++i;
+      cost = !strcmp(argv[i], "sad") ? ME_COST_SAD : !strcmp(argv[i], "ssim") ? ME_COST_SSIM : ME_COST_SSD;
     } else if (!strcmp(argv[i], "--gpus") && i + 1 < argc) {
       gpus = atoi(argv[++i]);
     } else if (!strcmp(argv[i], "--mv") && i + 1 < argc) {
@@ -102,7 +105,18 @@ int main(int argc, char** argv) {
     me_destroy(ctx);
     return 1;
   }
-  printf("PSNR: %.6f\n", psnr);
+  if (cost == ME_COST_SSIM) {
+    /* main_ssim.c:83-96: float sums of squared differences, pixel order */
+    float comp = 0.0f, orig = 0.0f;
+    for (size_t i = 0; i < n; i++) {
+      const int m = out[2 * n + i], c = out[n + i], r = out[i];
+      comp += (m - c) * (m - c);
+      orig += (c - r) * (c - r);
+    }
+    printf("Original Score: %.4f, Compensated Score: %.4f\n", orig / (int)n, comp / (int)n);
+  } else {
+    printf("PSNR: %.6f\n", psnr);
+  }
   printf("Output file dimensions: (%d x %d)\n", W, 5 * H);
   char path[4096];
   snprintf(path, sizeof path, "%s/output_%d_%d.yuv", pos[2], blk, span);
@@ -111,7 +125,7 @@ int main(int argc, char** argv) {
   if (mv_path && me_mv_write(mv_path, W, H, blk, span, cost, NULL, 1, mv, bc) != ME_OK)
     printf("Error: could not write %s\n", mv_path);
   printf("Computation time: %.lf ms\n", (t1 - t0) * 1000);
-  printf("PSNR: %.lf \n", psnr);
+  if (cost != ME_COST_SSIM) printf("PSNR: %.lf \n", psnr);
   me_destroy(ctx);
   free(mv);
   free(bc);

@@ -9,7 +9,7 @@
  *     --layout luma|i420   frame layout in the file (default luma: W*H per frame)
  *     --frames N           first N frames (default: all whole frames)
  *     --ref prev|first     pair k = (k, k+1) (default) or (0, k+1)
- *     --cost ssd|sad       default ssd (the reference's MSE choice)
+ *     --cost ssd|sad|ssim  default ssd (the reference's MSE choice)
  *     --gpus N             devices 0..N-1, pairs split in contiguous runs
  *     --repeat R           time R calls after a warm-up call (default 1)
  *     --mv FILE            write the MV fields + costs (MEMV, include/me.h)
@@ -43,7 +43,8 @@ int main(int argc, char** argv) {
     } else if (!strcmp(argv[i], "--ref") && i + 1 < argc) {
       first_ref = !strcmp(argv[++i], "first");
     } else if (!strcmp(argv[i], "--cost") && i + 1 < argc) {
-      cost = !strcmp(argv[++i], "sad") ? ME_COST_SAD : ME_COST_SSD;
+      ++i;
+      cost = !strcmp(argv[i], "sad") ? ME_COST_SAD : !strcmp(argv[i], "ssim") ? ME_COST_SSIM : ME_COST_SSD;
     } else if (!strcmp(argv[i], "--gpus") && i + 1 < argc) {
       gpus = atoi(argv[++i]);
     } else if (!strcmp(argv[i], "--repeat") && i + 1 < argc) {
@@ -56,7 +57,7 @@ int main(int argc, char** argv) {
   }
   if (npos < 5) {
     printf("Usage: mes_seq <sequence.yuv> <width> <height> <blk> <span> [--layout luma|i420] "
-           "[--frames N] [--ref prev|first] [--cost ssd|sad] [--gpus N] [--repeat R] [--mv FILE]\n");
+           "[--frames N] [--ref prev|first] [--cost ssd|sad|ssim] [--gpus N] [--repeat R] [--mv FILE]\n");
     return 1;
   }
   const int W = atoi(pos[1]), H = atoi(pos[2]), blk = atoi(pos[3]), span = atoi(pos[4]);
@@ -119,7 +120,7 @@ int main(int argc, char** argv) {
   const double per_call = (t1 - t0) / repeat;
   const double cand = (double)me_candidate_count(W, H, blk, span) * npairs;
   printf("Frames: %d, pairs: %d (%s), %dx%d, blk %d, span %d, %s, gpus %d\n", nframes, npairs,
-         first_ref ? "first" : "prev", W, H, blk, span, cost == ME_COST_SAD ? "sad" : "ssd", gpus);
+         first_ref ? "first" : "prev", W, H, blk, span, cost == ME_COST_SAD ? "sad" : cost == ME_COST_SSIM ? "ssim" : "ssd", gpus);
   printf("Computation time: %.3f ms per sequence (%.1f pairs/s, %.3e candidates/s incl. upload)\n",
          per_call * 1e3, npairs / per_call, cand / per_call);
   if (mv_path) {
