@@ -4,7 +4,9 @@
 //
 // The reference maximises a float SSIM score per candidate (first strict
 // maximum above 0 in raster order).  Every float operation is replayed in the
-// reference's order with round-to-nearest intrinsics (no contraction):
+// reference's order with round-to-nearest intrinsics, and the file is built
+// with -ffp-contract=off (csrc/Makefile: the intrinsics are plain operators
+// here, and a fused d*d + v rounds once where the reference rounds twice):
 //   mean   = (float) sum(p) / (float)(w*h)       sum of ints is exact in float
 //   var    = float chain sum((float)p - mean)^2 in raster order, / (w*h)
 //   cross  = float chain of int products (p - (int)mean_r)(c - (int)mean_c)
