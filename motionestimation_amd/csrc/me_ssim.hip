@@ -19,9 +19,10 @@
 // above 0 get MV (0, 0) and cost 0 (the reference leaves them uninitialised).
 // block_cost carries the float bits of the best score.
 //
-// One workgroup per block, one candidate per lane per step; the block and
-// its window are staged in LDS when they fit.  Float-latency bound (two
-// dependent w*h chains per candidate), not a hot path of the headline metric.
+// One workgroup per block, SSIM_Q adjacent candidates per lane per step; the
+// block and its window are staged in LDS when they fit.  Float-chain bound
+// (two dependent w*h chains per candidate, 2*SSIM_Q of them interleaved per
+// lane), not a hot path of the headline metric.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -32,6 +33,7 @@ namespace me {
 namespace {
 
 constexpr int SSIM_THREADS = 256;
+constexpr int SSIM_Q = 4;  // adjacent candidates per lane
 
 __device__ __forceinline__ uint64_t wave_min(uint64_t v) {
 #pragma unroll
@@ -103,33 +105,81 @@ __global__ __launch_bounds__(SSIM_THREADS) void me_ssim_kernel(SearchArgs p, int
   const float sp = sqrt_via_double(vp);
   const int imp = (int)mp;  // truncation, as the int parameter of computeCrossVar
 
+  // Lane = Q horizontally adjacent candidates: one cur byte and one ref byte
+  // per pixel step feed all Q (a sliding register window of ref bytes), and
+  // the 2Q float chains are independent (each still in raster order).
   uint64_t best = ~0ull;
-  const int ncand = ncx * ncy;
-  for (int t = tid; t < ncand; t += SSIM_THREADS) {
-    const int cy = t / ncx, cx = t - cy * ncx;
-    const uint8_t* r = staged ? win + cy * ww + cx
-                              : p.ref + (ptrdiff_t)(wy0 + cy - p.ref_row0) * p.stride + wx0 + cx;
+  const int ngx = (ncx + SSIM_Q - 1) / SSIM_Q;
+  const int ngroups = ngx * ncy;
+  for (int t = tid; t < ngroups; t += SSIM_THREADS) {
+    const int cy = t / ngx, cx0 = (t - cy * ngx) * SSIM_Q;
+    const uint8_t* r = staged ? win + cy * ww + cx0
+                              : p.ref + (ptrdiff_t)(wy0 + cy - p.ref_row0) * p.stride + wx0 + cx0;
     const int rp = staged ? ww : p.stride;
-    float mr, vr;
-    patch_stats(r, rp, w, h, nf, &mr, &vr);
-    const float sr = sqrt_via_double(vr);
-    const int imr = (int)mr;
-    float cv = 0.f;
-    for (int y = 0; y < h; y++)
-      for (int x = 0; x < w; x++)
-        cv = __fadd_rn(cv, (float)((r[y * rp + x] - imr) * (cblk[y * w + x] - imp)));
-    cv = __fdiv_rn(cv, nf);
-    const float lum = __fdiv_rn(__fadd_rn(__fmul_rn(__fmul_rn(2.f, mr), mp), C1),
-                                __fadd_rn(__fadd_rn(__fmul_rn(mr, mr), __fmul_rn(mp, mp)), C1));
-    const float con = __fdiv_rn(__fadd_rn(__fmul_rn(__fmul_rn(2.f, sr), sp), C2),
-                                __fadd_rn(__fadd_rn(__fmul_rn(sr, sr), __fmul_rn(sp, sp)), C2));
-    const float str = __fdiv_rn(__fadd_rn(cv, C3), __fadd_rn(__fmul_rn(sr, sp), C3));
-    const float score = __fmul_rn(__fmul_rn(lum, con), str);
-    if (score > 0.f) {
-      const int dx = wx0 + cx - tlx, dy = wy0 + cy - tly;
-      const uint64_t key = ((uint64_t)(0x7FFFFFFFu - __float_as_uint(score)) << 32) |
-                           ((uint32_t)(dy + 32768) << 16) | (uint32_t)(dx + 32768);
-      best = key < best ? key : best;
+    // Columns past the window (candidates cx0 + k >= ncx of the last group)
+    // are read but never used: padded in LDS, clamped in global memory.
+    const int lim = staged ? 0x7FFFFFFF : ww - 1 - cx0;
+    auto rb = [&](int y, int x) -> int { return r[y * rp + min(x, lim)]; };
+
+    int s[SSIM_Q];
+#pragma unroll
+    for (int k = 0; k < SSIM_Q; k++) s[k] = 0;
+    for (int y = 0; y < h; y++) {
+      int rw[SSIM_Q];
+#pragma unroll
+      for (int k = 0; k < SSIM_Q - 1; k++) rw[k + 1] = rb(y, k);
+      for (int x = 0; x < w; x++) {
+#pragma unroll
+        for (int k = 0; k < SSIM_Q - 1; k++) rw[k] = rw[k + 1];
+        rw[SSIM_Q - 1] = rb(y, x + SSIM_Q - 1);
+#pragma unroll
+        for (int k = 0; k < SSIM_Q; k++) s[k] += rw[k];
+      }
+    }
+    float mr[SSIM_Q], vr[SSIM_Q], cv[SSIM_Q];
+    int imr[SSIM_Q];
+#pragma unroll
+    for (int k = 0; k < SSIM_Q; k++) {
+      mr[k] = __fdiv_rn((float)s[k], nf);
+      imr[k] = (int)mr[k];
+      vr[k] = 0.f;
+      cv[k] = 0.f;
+    }
+    for (int y = 0; y < h; y++) {
+      int rw[SSIM_Q];
+#pragma unroll
+      for (int k = 0; k < SSIM_Q - 1; k++) rw[k + 1] = rb(y, k);
+      for (int x = 0; x < w; x++) {
+#pragma unroll
+        for (int k = 0; k < SSIM_Q - 1; k++) rw[k] = rw[k + 1];
+        rw[SSIM_Q - 1] = rb(y, x + SSIM_Q - 1);
+        const int cc = cblk[y * w + x] - imp;
+#pragma unroll
+        for (int k = 0; k < SSIM_Q; k++) {
+          const float d = __fsub_rn((float)rw[k], mr[k]);
+          vr[k] = __fadd_rn(vr[k], __fmul_rn(d, d));
+          cv[k] = __fadd_rn(cv[k], (float)((rw[k] - imr[k]) * cc));
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < SSIM_Q; k++) {
+      if (cx0 + k >= ncx) break;
+      const float sr = sqrt_via_double(__fdiv_rn(vr[k], nf));
+      const float cvk = __fdiv_rn(cv[k], nf);
+      const float m = mr[k];
+      const float lum = __fdiv_rn(__fadd_rn(__fmul_rn(__fmul_rn(2.f, m), mp), C1),
+                                  __fadd_rn(__fadd_rn(__fmul_rn(m, m), __fmul_rn(mp, mp)), C1));
+      const float con = __fdiv_rn(__fadd_rn(__fmul_rn(__fmul_rn(2.f, sr), sp), C2),
+                                  __fadd_rn(__fadd_rn(__fmul_rn(sr, sr), __fmul_rn(sp, sp)), C2));
+      const float str = __fdiv_rn(__fadd_rn(cvk, C3), __fadd_rn(__fmul_rn(sr, sp), C3));
+      const float score = __fmul_rn(__fmul_rn(lum, con), str);
+      if (score > 0.f) {
+        const int dx = wx0 + cx0 + k - tlx, dy = wy0 + cy - tly;
+        const uint64_t key = ((uint64_t)(0x7FFFFFFFu - __float_as_uint(score)) << 32) |
+                             ((uint32_t)(dy + 32768) << 16) | (uint32_t)(dx + 32768);
+        best = key < best ? key : best;
+      }
     }
   }
   best = wave_min(best);
@@ -159,9 +209,10 @@ hipError_t launch_ssim(const SearchArgs& p, hipStream_t stream) {
   const int B = p.blk;
   long win = (long)(B + 2 * p.range) * (B + 2 * p.range);
   const int cur = (B * B + 15) & ~15;
-  if (cur + win > GENERIC_LDS_BUDGET) win = 0;  // read the window from global memory
+  if (cur + win + SSIM_Q > GENERIC_LDS_BUDGET) win = 0;  // read the window from global memory
+  // + SSIM_Q bytes: the last candidate group of the last row reads past the window
   hipLaunchKernelGGL(me_ssim_kernel, dim3((unsigned)(rows * p.nbx)), dim3(SSIM_THREADS),
-                     cur + (int)win, stream, p, p.block_row_begin, (int)win);
+                     cur + (int)win + SSIM_Q, stream, p, p.block_row_begin, (int)win);
   return hipGetLastError();
 }
 
