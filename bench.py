@@ -91,7 +91,14 @@ def cpu_baselines(ref, cur, blk, span, cost, threads, cands):
         O.full_search(ref, cur, blk, span, cost, threads=threads, begin=begin, end=end)
         times.append(time.perf_counter() - t0)
     med = statistics.median(times)
+    cpu_model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            cpu_model = next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), "")
+    except OSError:
+        pass
     out = {"value": cands / med, "unit": "candidates/s", "cores": threads, "kind": "port",
+           "cpu_model": cpu_model, "host_cpus": os.cpu_count(),
            "sample": f"{what} {w}x{h} B{blk} +-{span} {cost.upper()} frame, "
                      f"oracle/me_oracle.c -O2, {threads} pthreads, median of 5 ({med*1e3:.1f} ms)"}
     mes = os.path.join(REPO, "oracle", "_ref", "mes")
