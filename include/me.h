@@ -70,6 +70,7 @@ typedef enum {
 /* Limits of this build. */
 #define ME_MAX_BLOCK 64    /* block_size in [1, 64]  (SSD of 64x64 < 2^32) */
 #define ME_MAX_RANGE 1024  /* search_range in [0, 1024] */
+/* stride * height < 2^31 bytes per plane (ME_EUNSUPPORTED otherwise). */
 
 typedef struct me_ctx me_ctx;
 

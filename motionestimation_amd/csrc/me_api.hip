@@ -54,6 +54,10 @@ me_status check_args(me_ctx* c, const void* ref, const void* cur, int width, int
   if (range < 0 || range > ME_MAX_RANGE) return fail(c, ME_EINVAL, "search_range %d", range);
   if (cost != ME_COST_SSD && cost != ME_COST_SAD && cost != ME_COST_SSIM)
     return fail(c, ME_EINVAL, "cost %d", cost);
+  // Buffer descriptors carry 32-bit byte ranges: planes stay below 2 GiB.
+  if ((long long)stride * height >= (1LL << 31))
+    return fail(c, ME_EUNSUPPORTED, "plane of %lld bytes (limit 2 GiB)",
+                (long long)stride * height);
   return ME_OK;
 }
 

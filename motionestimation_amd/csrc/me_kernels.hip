@@ -871,9 +871,12 @@ bool plan_fast(const SearchArgs& p, QsadGeom* g, int* k_out) {
             cost += (many ? (t + 63) / 64 : rounds * (thr / 64) + 0.5 * (rounds - 1)) + 0.45;
             useful += t / 64.0;
           }
-          // too few work items leave workgroup slots idle (and nothing to
-          // prefetch): aim for >= 2 items per resident workgroup (4 per CU).
-          const double fill = items >= 2048 ? 1.0 : (double)items / 2048;
+          // Workgroups take whole tiles (every pass of a tile runs on the
+          // workgroup holding its keys): too few tiles leave workgroup slots
+          // idle (and nothing to prefetch): aim for >= 2 tiles per resident
+          // workgroup (4 per CU).
+          const long tiles = items / passes;
+          const double fill = tiles >= 2048 ? 1.0 : (double)tiles / 2048;
           // K = 13 measured best wherever it fits (more candidates per row load
           // and per epilogue than the padding it costs).
           const double kpref = K == 13 ? 1.0 : 0.95;

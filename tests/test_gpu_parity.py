@@ -192,6 +192,11 @@ def test_error_paths(engine):
         assert ei.value.status == me._lib.ME_EINVAL
     with pytest.raises(me.MEError):
         engine.full_search(ref, ref, 8, 4, "nope")
+    # planes of 2 GiB or more are refused before any device work
+    st = me._lib.lib().me_full_search(engine._h, ref.ctypes.data, ref.ctypes.data, 32, 32,
+                                      1 << 26, 8, 4, me.ME_COST_SAD,
+                                      np.zeros(64, np.int16).ctypes.data, None)
+    assert st == me._lib.ME_EUNSUPPORTED
 
 
 @pytest.mark.slow
