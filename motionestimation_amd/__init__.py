@@ -10,5 +10,6 @@ from .engine import (Engine, candidate_count, num_blocks, pinned_frames,  # noqa
                      plan_stripes, version)
 from . import io  # noqa: F401
 from .reference_api import (Block, PredictionFrame, create_prediction_frame,  # noqa: F401
-                            find_best_blk_mse, find_best_blks, frame_diff,
+                            find_best_blk_mse, find_best_blk_ssim, find_best_blks,
+                            frame_diff,
                             motion_compensated_frame, output_planes)

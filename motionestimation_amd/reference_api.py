@@ -6,6 +6,7 @@ Reference (souravBhat/MotionEstimation):
   predictionFrame              src/common/prediction_frame.h:8-16
   createPredictionFrame        src/common/prediction_frame.c:3-25
   findBestBlkMse (per block)   src/cpu/main.c:67-82  -> find_best_blk_mse
+  findBestBlkSSIM (per block)  src/cpu/main_ssim.c:15-29 -> find_best_blk_ssim
   thread-pool dispatch         src/cpu/main.c:144-158 -> find_best_blks (whole frame)
   motionCompensatedFrame       src/common/utils.c:102-134
   frameDiff / imagePSNR        src/common/utils.c:94-100 / :137-164
@@ -77,8 +78,9 @@ def find_best_blks(pf: PredictionFrame, reference_frame, extra_span: int, cost="
                    engine=None) -> np.ndarray:
     """All blocks of pf at once (the thread-pool loop of main.c:144-158).
     Fills motion_vectorX/Y and is_best_match_found = 1 on every block and
-    returns the per-block MSE (SSD / (w*h) as float32, the reference's score)
-    or SAD."""
+    returns the per-block MSE (SSD / (w*h) as float32, the reference's score),
+    SAD, or for cost="ssim" the reference's SSIM score (float32; 0 with MV
+    (0, 0) where no candidate scores above 0, ssim.c:87-104)."""
     ref = np.asarray(reference_frame).reshape(pf.height, pf.width).astype(np.uint8)
     cur = np.asarray(pf.frame).reshape(pf.height, pf.width).astype(np.uint8)
     mv, cst = _engine(engine).full_search(ref, cur, pf.blk_dim, extra_span, cost)
@@ -87,6 +89,8 @@ def find_best_blks(pf: PredictionFrame, reference_frame, extra_span: int, cost="
     if cost in ("ssd", "mse", 0):
         area = np.array([b.width * b.height for b in pf.blks], np.float32)
         return cst.astype(np.float32) / area
+    if cost in ("ssim", 2):
+        return cst.view(np.float32)
     return cst
 
 
@@ -95,6 +99,18 @@ def find_best_blk_mse(pf: PredictionFrame, reference_frame, blk: Block, extra_sp
     """findBestBlkMse for one block (kept for interface parity; it searches the
     frame on the GPU and picks this block's result)."""
     scores = find_best_blks(pf, reference_frame, extra_span, "ssd", engine)
+    i = blk.idx_y * ((pf.width + pf.blk_dim - 1) // pf.blk_dim) + blk.idx_x
+    src = pf.blks[i]
+    blk.motion_vectorX, blk.motion_vectorY = src.motion_vectorX, src.motion_vectorY
+    blk.is_best_match_found = 1
+    return float(scores[i])
+
+
+def find_best_blk_ssim(pf: PredictionFrame, reference_frame, blk: Block, extra_span: int,
+                       engine=None) -> float:
+    """findBestBlkSSIM for one block (main_ssim.c:15-29): the best SSIM score,
+    MV written into blk (the search runs over the frame on the GPU)."""
+    scores = find_best_blks(pf, reference_frame, extra_span, "ssim", engine)
     i = blk.idx_y * ((pf.width + pf.blk_dim - 1) // pf.blk_dim) + blk.idx_x
     src = pf.blks[i]
     blk.motion_vectorX, blk.motion_vectorY = src.motion_vectorX, src.motion_vectorY

@@ -74,3 +74,18 @@ def test_ssim_c_driver_matches_reference_driver(tmp_path, manifest):
         assert d["score_line"] in r.stdout, r.stdout
         out = (tmp_path / f"output_{d['blk']}_{d['span']}.yuv").read_bytes()
         assert hashlib.sha256(out).hexdigest() == d["output_sha256"]
+
+
+def test_ssim_reference_interface(engine, manifest):
+    """find_best_blks(cost='ssim') / find_best_blk_ssim mirror main_ssim.c:15-29."""
+    f1, f2 = O.load_frame("ForemanYF1", manifest), O.load_frame("ForemanYF2", manifest)
+    c = [c for c in manifest["ssim_cases"] if c["name"] == "ssim_foreman21_b16_s7"][0]
+    gmv, gscore = O.load_case(c)
+    pf = me.create_prediction_frame(f2, 352, 288, 16)
+    scores = me.find_best_blks(pf, f1, 7, cost="ssim", engine=engine)
+    np.testing.assert_array_equal(scores.view(np.uint32), gscore.view(np.uint32))
+    np.testing.assert_array_equal(me.reference_api.mv_field(pf).astype(np.int32), gmv)
+    blk = pf.blks[57]
+    s = me.find_best_blk_ssim(pf, f1, blk, 7, engine=engine)
+    assert np.float32(s).view(np.uint32) == gscore.view(np.uint32)[57]
+    assert [blk.motion_vectorX, blk.motion_vectorY] == gmv[57].tolist()
