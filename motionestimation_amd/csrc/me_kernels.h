@@ -50,6 +50,7 @@ struct QsadGeom {
   int aligned;     // 4-byte aligned global rows
   int fold;        // SAD, S % 4 == 0: groups = S/2 cover dx in [-S, S-1]; the dx = +S
                    // column is spread over lanes gi < K, one v_sad_u8 candidate each
+  int dyn_tiles;   // dynamic tile pulls when tiles >= dyn_tiles * workgroups (0: never)
 };
 
 hipError_t launch_search(const SearchArgs& p, hipStream_t stream, int* used_fast);

@@ -549,29 +549,44 @@ __global__ __launch_bounds__(1024) void me_fast_kernel(SearchArgs p, QsadGeom g)
   const int n_x = nwg / ng + (x < nwg % ng ? 1 : 0);
   const int band0 = (int)((long)ntiles * x / ng), band1 = (int)((long)ntiles * (x + 1) / ng);
   const int passes = (g.chunks + g.cpp - 1) / g.cpp;
-  // Dynamic only with many tiles per workgroup: with few, the two-ahead pulls
-  // hand out every tile at the start (random order) and balance worse than
-  // round-robin; with many, pulls follow CU speed (8K: -7 % time).
-  const bool dyn = p.sched != nullptr && ntiles >= 8 * nwg;
+  // Dynamic only with enough tiles per workgroup (g.dyn_tiles, see plan_fast):
+  // with few, the item-start pulls of all workgroups coincide and serialise.
+  const bool dyn = p.sched != nullptr && g.dyn_tiles > 0 && ntiles >= g.dyn_tiles * nwg;
   int* tq = reinterpret_cast<int*>(smem + 2 * buf_bytes + 128);  // 4-slot ring of tile ids
 #ifdef ME_STAMPS
   const int wid = bid;
 #endif
   ME_STAMP(0, __builtin_amdgcn_s_memtime());
   ME_STAMP(6, __builtin_amdgcn_s_memrealtime());
+  // Dynamic: each workgroup's first two tiles are its static ones (no atomic
+  // storm at launch); the counter of band y hands out the band's tiles past
+  // its first 2 * n_y.  Own band first; once it is exhausted, steal from the
+  // other XCD groups' bands (clocks differ by several % between XCDs, so
+  // bands finish unevenly).
   auto pull = [&]() -> int {
-    const uint32_t i = __hip_atomic_fetch_add(p.sched + x, 1u, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
-    return (int)i < band1 - band0 ? band0 + (int)i : -1;
+    for (int d = 0; d < ng; d++) {
+      const int y = x + d < ng ? x + d : x + d - ng;
+      const int b0 = (int)((long)ntiles * y / ng), b1 = (int)((long)ntiles * (y + 1) / ng);
+      const int n_y = nwg / ng + (y < nwg % ng ? 1 : 0);
+      const int first = min(b1 - b0, 2 * n_y);
+      const uint32_t i = __hip_atomic_fetch_add(p.sched + y, 1u, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+      if ((int)i < b1 - b0 - first) return b0 + first + (int)i;
+    }
+    return -1;
   };
-  auto tile_at = [&](int i) -> int {  // i-th tile of this workgroup, -1 = none
-    if (dyn) return tq[i & 3];
+  auto static_tile = [&](int i) -> int {  // i-th static tile of this workgroup
     const int t = band0 + m + i * n_x;
     return t < band1 ? t : -1;
   };
+  auto tile_at = [&](int i) -> int {  // i-th tile of this workgroup, -1 = none
+    return dyn ? tq[i & 3] : static_tile(i);
+  };
   if (dyn && tid == 0) {
-    tq[0] = pull();
-    tq[1] = tq[0] >= 0 ? pull() : -1;
+    tq[0] = static_tile(0);
+    if (tq[0] < 0) tq[0] = pull();
+    tq[1] = static_tile(1);
+    if (tq[1] < 0 && tq[0] >= 0) tq[1] = pull();
   }
   if (tid < g.tb) keys[tid] = ~0ull;
   __syncthreads();
@@ -895,6 +910,20 @@ bool plan_fast(const SearchArgs& p, QsadGeom* g, int* k_out) {
   if (best < 0) return false;  // nothing fits (only with an ME_PLAN override)
   g->fold = bF;
   g->groups = bG;
+  // Dynamic tile pulls from this many tiles per workgroup on (ME_DYN overrides
+  // for tuning; 0 = static bands only).
+  {
+    static int dyn_env = -2;
+    if (dyn_env == -2) {
+      const char* e = getenv("ME_DYN");
+      dyn_env = e ? atoi(e) : -1;
+    }
+    // 3: measured (tools/dyn_sweep.sh) -- 4K (3.96 tiles/WG) and 8K gain
+    // (8K -11 % with stealing), 1080p (2.7 tiles/WG) loses: its workgroups
+    // start items in lockstep and the item-start pulls serialise on the
+    // device-scope counters while wave 0 waits.
+    g->dyn_tiles = dyn_env >= 0 ? dyn_env : 3;
+  }
   g->tb = bTB;
   g->cpp = bC;
   g->chunks = (D + bK - 1) / bK;
