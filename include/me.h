@@ -89,6 +89,14 @@ const char* me_last_error(const me_ctx* ctx);
 /* Library version string, e.g. "me_hip 1 gfx950". */
 const char* me_version(void);
 
+/* Kernel path (process-wide; A/B tests and diagnostics).  ME_PATH_AUTO: SSD
+ * searches with 16x16 blocks run on the matrix cores (i8 MFMA), everything
+ * else on the VALU kernels; ME_PATH_VALU: VALU kernels only.  Results are
+ * identical either way.  The environment variable ME_PATH=valu sets the
+ * initial value. */
+typedef enum { ME_PATH_AUTO = 0, ME_PATH_VALU = 1 } me_path;
+void me_set_kernel_path(me_path path);
+
 /* Tiling helpers (src/common/prediction_frame.c:9-11). */
 int me_num_blocks(int width, int height, int block_size);
 /* Exact number of candidates the search evaluates (reference clamping). */

@@ -18,6 +18,7 @@ CSRC = os.path.join(PKG, "csrc")
 ME_OK, ME_EINVAL, ME_ENOMEM, ME_EDEVICE, ME_ECOMM, ME_EUNSUPPORTED, ME_EIO = range(7)
 ME_YUV_LUMA, ME_YUV_I420 = 0, 1
 ME_COST_SSD, ME_COST_SAD, ME_COST_SSIM = 0, 1, 2
+ME_PATH_AUTO, ME_PATH_VALU = 0, 1
 ME_MAX_BLOCK, ME_MAX_RANGE = 64, 1024
 
 # Every symbol include/me.h declares, with (restype, argtypes).
@@ -30,6 +31,7 @@ _SIGS = {
     "me_last_error": (ctypes.c_char_p, [ctypes.c_void_p]),
     "me_version": (ctypes.c_char_p, []),
     "me_num_blocks": (ctypes.c_int, [ctypes.c_int] * 3),
+    "me_set_kernel_path": (None, [ctypes.c_int]),
     "me_candidate_count": (ctypes.c_uint64, [ctypes.c_int] * 4),
     "me_full_search": (ctypes.c_int, [ctypes.c_void_p, _u8p, _u8p] + [ctypes.c_int] * 6 +
                        [ctypes.c_void_p, ctypes.c_void_p]),

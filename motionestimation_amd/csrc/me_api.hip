@@ -88,7 +88,21 @@ SearchArgs make_args(const uint8_t* ref, int ref_row0, const uint8_t* cur, int c
   p.ref_bytes = ref_rows > 0 ? (uint32_t)((ref_rows - 1) * (long)stride + width) : 0;
   p.cur_bytes = cur_rows > 0 ? (uint32_t)((cur_rows - 1) * (long)stride + width) : 0;
   p.sched = nullptr;
+  p.scratch = nullptr;
+  p.scratch_bytes = 0;
   return p;
+}
+
+me_status attach_scratch(me_ctx* c, Dev& d, SearchArgs& p) {
+  p.sched = d.sched;
+  const size_t need = mfma_ssd_scratch(p);
+  if (need) {
+    me_status s = grow(c, (void**)&d.scratch, &d.scratch_cap, need);
+    if (s != ME_OK) return s;
+  }
+  p.scratch = d.scratch;
+  p.scratch_bytes = d.scratch ? d.scratch_cap : 0;
+  return ME_OK;
 }
 
 }  // namespace me
@@ -99,6 +113,7 @@ using me::fail;
 using me::grow;
 using me::check_args;
 using me::make_args;
+using me::attach_scratch;
 
 uint64_t row_candidates(int width, int height, int blk, int range, int by) {
   const int nbx = (width + blk - 1) / blk;
@@ -172,7 +187,7 @@ me_status multi_search(me_ctx* c, const uint8_t* ref, const uint8_t* cur, int wi
     uint32_t* dcost = reinterpret_cast<uint32_t*>(d.rec + max_blocks * 4);
     me::SearchArgs p = make_args(d.ref, y_ref0, d.cur, y_cur0, width, height, width, blk, range,
                                  cost, r0, r1, dmv, dcost);
-    p.sched = d.sched;
+    if ((s = attach_scratch(c, d, p)) != ME_OK) return s;
     HIPCHK(c, me::launch_search(p, d.stream, nullptr));
   }
   Dev& root = c->devs[0];
@@ -234,6 +249,8 @@ const char* me_status_str(me_status s) {
 const char* me_last_error(const me_ctx* ctx) { return ctx ? ctx->err : "null context"; }
 
 const char* me_version(void) { return "me_hip 1 gfx950"; }
+
+void me_set_kernel_path(me_path path) { me::set_force_valu(path == ME_PATH_VALU ? 1 : 0); }
 
 int me_num_blocks(int width, int height, int blk) {
   if (width <= 0 || height <= 0 || blk <= 0) return 0;
@@ -329,6 +346,7 @@ void me_destroy(me_ctx* c) {
     (void)hipFree(d.stats);
     (void)hipFree(d.out5);
     (void)hipFree(d.sched);
+    (void)hipFree(d.scratch);
     me::release_pipeline(d);
     if (d.stream) (void)hipStreamDestroy(d.stream);
   }
@@ -357,7 +375,7 @@ me_status me_full_search(me_ctx* c, const uint8_t* ref, const uint8_t* cur, int 
   const int nby = (height + blk - 1) / blk;
   me::SearchArgs p = make_args(d.ref, 0, d.cur, 0, width, height, width, blk, range, cost, 0,
                                nby, dmv, dcost);
-  p.sched = d.sched;
+  if ((s = attach_scratch(c, d, p)) != ME_OK) return s;
   HIPCHK(c, me::launch_search(p, d.stream, nullptr));
   HIPCHK(c, hipMemcpyAsync(mv_xy, dmv, nb * 4, hipMemcpyDeviceToHost, d.stream));
   if (block_cost)
@@ -381,7 +399,7 @@ me_status me_full_search_stripe_device(me_ctx* c, const uint8_t* d_ref, int ref_
   c->err[0] = 0;
   me::SearchArgs p = make_args(d_ref, ref_row0, d_cur, cur_row0, width, height, stride, blk,
                                range, cost, r0, r1, d_mv, d_cost);
-  p.sched = c->devs[0].sched;
+  if ((s = attach_scratch(c, c->devs[0], p)) != ME_OK) return s;
   HIPCHK(c, me::launch_search(p, (hipStream_t)stream, nullptr));
   return ME_OK;
 }

@@ -29,6 +29,8 @@ struct Dev {
   uint8_t* out5 = nullptr;
   size_t out_cap = 0;
   uint32_t* sched = nullptr;  // fast-kernel tile counters (self-resetting)
+  uint8_t* scratch = nullptr; // MFMA SSD prepass planes (me_mfma.hip), grown on demand
+  size_t scratch_cap = 0;
   // Frame-pair pipeline (me_stream.hip), kept across calls.
   std::vector<uint8_t*> slots;        // device frames, slot_bytes each
   std::vector<hipEvent_t> slot_ready; // upload of the slot's frame done (copy stream)
@@ -51,6 +53,11 @@ me_status check_args(me_ctx* c, const void* ref, const void* cur, int width, int
 SearchArgs make_args(const uint8_t* ref, int ref_row0, const uint8_t* cur, int cur_row0,
                      int width, int height, int stride, int blk, int range, int cost, int r0,
                      int r1, int16_t* mv, uint32_t* cst);
+
+// Point p at d's search scratch, growing it to what p's search needs.  A
+// device's scratch serves one search at a time: searches of one context are
+// stream-ordered (one stream per device, or the caller's stream).
+me_status attach_scratch(me_ctx* c, Dev& d, SearchArgs& p);
 
 // Pinned host ranges handed out by me_host_alloc (the pair pipeline DMAs
 // straight from them instead of staging).

@@ -29,6 +29,8 @@ struct SearchArgs {
   uint32_t ref_bytes;  // readable bytes from ref (buffer range check), and from cur
   uint32_t cur_bytes;
   uint32_t* sched;     // 9 zeroed u32 (8 XCD-group tile counters + arrivals) or null
+  uint8_t* scratch;    // device scratch of the MFMA SSD path (mfma_ssd_scratch bytes) or null
+  size_t scratch_bytes;
 };
 
 struct QsadGeom {
@@ -52,6 +54,32 @@ struct QsadGeom {
                    // column is spread over lanes gi < K, one v_sad_u8 candidate each
   int dyn_tiles;   // dynamic tile pulls when tiles >= dyn_tiles * workgroups (0: never)
 };
+
+// Matrix-core SSD path (me_mfma.hip): B = 16, full-height rows [row0, row0 +
+// nrows) x full-width columns [0, nbx); 4x4-block tiles.
+struct MfmaGeom {
+  int row0, nrows, nbx;
+  int tiles_x, tiles_y;
+  int ngx;               // 64-position groups per tile row of candidates (waves = 4 ngx)
+  int km;                // candidate rows per chunk L = 13 + 16 km
+  int lds;               // dynamic LDS bytes
+  int hb, hb_row;        // partial bottom block row: height hb, block row index (-1: none)
+  int ya0, rp_rows;      // frame rows [ya0, ya0 + rp_rows) of the prepass planes
+  int rows_alloc;        // plane rows written (rp_rows + read slack)
+  int pitch;             // row pitch of the planes (entries)
+  int s2h_row0;          // first s2h row the kernel reads
+  uint32_t rp_bytes, s2_bytes;  // buffer ranges (s2_bytes spans s2 and s2h)
+  uint32_t s2h_off;      // byte offset of s2h from s2
+  size_t scratch_bytes;
+  int8_t* rp;            // ref ^ 0x80
+  int* s2;               // 16x16 box sums of (ref - 127)^2
+  int* s2h;              // hb x 16 box sums (partial bottom row only)
+};
+bool plan_mfma_ssd(const SearchArgs& p, MfmaGeom* g);
+hipError_t launch_mfma_ssd(const SearchArgs& p, const MfmaGeom& g, hipStream_t stream);
+size_t mfma_ssd_scratch(const SearchArgs& p);  // 0: path not applicable
+bool mfma_disabled();
+void set_force_valu(int v);  // 1: VALU kernels only, 0: automatic
 
 hipError_t launch_search(const SearchArgs& p, hipStream_t stream, int* used_fast);
 hipError_t launch_generic(const SearchArgs& p, int bx0, int nbx_range, int row0, int nrows,

@@ -1048,11 +1048,9 @@ static bool cached_plan(const SearchArgs& p, QsadGeom* g, int* K) {
   return e.ok;
 }
 
-hipError_t launch_search(const SearchArgs& p, hipStream_t stream, int* used_fast) {
+static hipError_t launch_valu(const SearchArgs& p, hipStream_t stream, int* used_fast) {
   const int r0 = p.block_row_begin, r1 = p.block_row_end;
   if (r1 <= r0) return hipSuccess;
-  if (used_fast) *used_fast = 0;
-  if (p.cost_kind == COST_SSIM) return launch_ssim(p, stream);
   QsadGeom g;
   int K = 0;
   if (!cached_plan(p, &g, &K)) return launch_generic(p, 0, p.nbx, r0, r1 - r0, stream);
@@ -1072,6 +1070,25 @@ hipError_t launch_search(const SearchArgs& p, hipStream_t stream, int* used_fast
   if (g.nbx_full < p.nbx)  // partial right column
     return launch_generic(p, g.nbx_full, p.nbx - g.nbx_full, r0, r1 - r0, stream);
   return hipSuccess;
+}
+
+hipError_t launch_search(const SearchArgs& p, hipStream_t stream, int* used_fast) {
+  const int r0 = p.block_row_begin, r1 = p.block_row_end;
+  if (r1 <= r0) return hipSuccess;
+  if (used_fast) *used_fast = 0;
+  if (p.cost_kind == COST_SSIM) return launch_ssim(p, stream);
+  MfmaGeom mg;
+  if (p.cost_kind == COST_SSD && p.scratch && plan_mfma_ssd(p, &mg) &&
+      p.scratch_bytes >= mg.scratch_bytes) {
+    // Matrix cores: every full-width block (the partial bottom row included);
+    // the partial right column stays on the generic kernel.
+    hipError_t e = launch_mfma_ssd(p, mg, stream);
+    if (e != hipSuccess) return e;
+    if (used_fast) *used_fast = 2;
+    if (mg.nbx < p.nbx) return launch_generic(p, mg.nbx, p.nbx - mg.nbx, r0, r1 - r0, stream);
+    return hipSuccess;
+  }
+  return launch_valu(p, stream, used_fast);
 }
 
 }  // namespace me

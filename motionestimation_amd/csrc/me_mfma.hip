@@ -1,0 +1,637 @@
+// me_mfma.hip -- the reference's cost (float MSE = SSD / (w*h), souravBhat/
+// MotionEstimation src/cpu/main.c:18-36) on the CDNA4 matrix cores, for 16x16
+// blocks.  SAD stays on the VALU (|a - b| is no contraction); SSD is one:
+//
+//   SSD(block m, candidate top-left (x, y))
+//     = sum (c - r)^2 = Cc_m + S2(x, y) + 2 X_m(x, y)
+//   c'' = 127 - c, r' = r - 128      (both in i8: bytes c ^ 0x7F and r ^ 0x80)
+//   X_m(x, y) = sum_{i,j} c''_m[i][j] * r'[y + i][x + j]   (v_mfma_i32_16x16x64_i8)
+//   Cc_m      = sum (c''^2 + 2 c'')  = sum (128 - c)^2 - 256     (per block)
+//   S2(x, y)  = sum (r - 127)^2 over the 16x16 window at (x, y)  (per position)
+// Everything is exact integer arithmetic, so the argmin (raster-first ties,
+// main.c:53-60) and the reported SSD are the VALU kernels' bit for bit, and
+// through them the reference's float-MSE choice.
+//
+// GEMM shape: M = 16 blocks of a 4x4 block tile, N = 16 candidate positions,
+// K = 64 = 4 block rows x 16 columns; four MFMAs (q = 0..3, block rows 4q..4q+3)
+// complete one 16x16 output tile (16 positions at one y, 16 blocks).  The B
+// operand of lane (n, h) is window row R + h at position x_n, and it feeds
+// the tiles y = R, R-4, R-8, R-12 (q = 0..3): one 16-byte LDS fragment per
+// four MFMAs.  Positions of a wave are x_n = xbase + 4n + s (stride 4): all
+// its lanes share the byte alignment of x_n, and the window is held in LDS as
+// four copies shifted by 0..3 bytes (LDS DMA from unaligned offsets, probed
+// exact on gfx950: tools/mfma_probe.hip), so every fragment read is dword
+// aligned and needs no realignment.
+//
+// Epilogue per output tile, per lane (position n, block row h, block column r
+// in result register r): 32-bit keys
+//   key = (SSD - p_m + 1) << 6 | (y - y0)          (p_m = Cc_m & 1)
+//       = ((S2 + 1) << 6) + (y - y0) + (acc << 7),   acc = X + Cc_m >> 1
+// so one v_lshl_add per candidate and an unsigned min.  Invalid pairs cannot
+// win: x out of block m's window -> acc starts 2^23 higher (key in [2^30,
+// 2^31)); y out of block row h's window -> bit 31 set on the lane's position
+// term.  The lane's best key per block is widened to the (cost, dy, dx) key of
+// the VALU kernels and merged with one LDS atomicMin per block per task.
+//
+// The window bytes r ^ 0x80 and the S2 plane come from a prepass kernel over
+// the reference plane (me_ssd_prep_kernel): 5 bytes per pixel of scratch.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdlib.h>
+
+#include <type_traits>
+
+#include "me_kernels.h"
+
+#ifndef ME_MFMA_ABLATE
+#define ME_MFMA_ABLATE 0  // diagnostic bit set (csrc/Makefile mablate, tools/mablate.sh); never shipped
+#endif
+
+namespace me {
+
+namespace {
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) const uint32_t lds_u32;
+
+template <int I, int N, typename F>
+__device__ __forceinline__ void sfor(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    sfor<I + 1, N>(f);
+  }
+}
+
+#ifdef ME_STAMPS
+// Diagnostic build only: per workgroup [start, staged, chunk 0 done, end,
+// hw_id, xcc_id, realtime start, realtime end] (tools/mfma_stamps.py).
+__device__ unsigned long long g_mstamps[8 << 14];
+#define MS_STAMP(slot, v) do { if (threadIdx.x == 0 && blockIdx.x < (1u << 14)) g_mstamps[8 * blockIdx.x + (slot)] = (v); } while (0)
+// prepass: [start, staged, rp done, end] per workgroup, after the main kernel's slots
+__device__ unsigned long long g_pstamps[6 << 14];
+#define PS_STAMP(slot) do { const unsigned b_ = blockIdx.y * gridDim.x + blockIdx.x; \
+  if (threadIdx.x == 0 && b_ < (1u << 14)) { g_pstamps[6 * b_ + (slot)] = __builtin_amdgcn_s_memtime(); \
+    if ((slot) == 0 || (slot) == 3) g_pstamps[6 * b_ + 4 + ((slot) == 3)] = __builtin_amdgcn_s_memrealtime(); } } while (0)
+#else
+#define MS_STAMP(slot, v) do { } while (0)
+#define PS_STAMP(slot) do { } while (0)
+#endif
+
+__device__ __forceinline__ int opaque(int v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
+// -------------------------------------------------------------- prepass
+// Plane row rr is frame row ya0 + rr; every plane holds rows_alloc rows of
+// `pitch` entries, all written (the main kernel's masked candidates read the
+// padding, and its keys stay ordered only while every S2 it reads is < 2^23):
+//   rp [rr][x]  = ref ^ 0x80 (the i8 value r - 128), 0 outside the frame
+//   s2 [rr][x]  = sum_{i < 16, j < 16} (ref[ya0 + rr + i][x + j] - 127)^2,
+//                 0 where the 16x16 window leaves the resident rows / frame
+//   s2h[rr][x]  = the same over hb rows (the partial bottom block row, block
+//                 height hb), rows >= s2h_row0 only (the last tile row's range)
+// One workgroup: 64 x 64 outputs from a 79 x 80 byte window in LDS.
+// Vertical sliding sums down each column into LDS (lanes on consecutive
+// columns: conflict-free), then horizontal sliding sums along each row in
+// registers, stored as 16 consecutive ints per thread.
+constexpr int PREP_W = 64 + 16;  // staged columns (64 + 15, dword padded)
+constexpr int PREP_R = 64 + 15;  // staged rows
+constexpr int VS_P = 84;         // ints per row of the vertical sums (16-byte rows, bank spread)
+
+__device__ __forceinline__ int sq127(int v) {
+  v -= 127;
+  return v * v;
+}
+
+// Vertical BH-row sums of one 16-row segment per task (every byte load
+// independent: one LDS latency per task), then horizontal 16-sums per
+// (row, 16 columns) in registers -> plane rows [row_lo, rows_alloc).
+template <int BH>
+__device__ __forceinline__ void box_pass(const MfmaGeom& g, const uint8_t* win, int* vs, int* plane,
+                                         int x0, int r0, int row_lo, int W) {
+  const int tid = (int)threadIdx.x;
+  __syncthreads();  // vs free (a previous pass read it)
+  for (int t = tid; t < PREP_W * 4; t += 256) {  // (column, 16-row segment)
+    const int x = t % PREP_W, y0 = 16 * (t / PREP_W);
+    const uint8_t* c = win + y0 * PREP_W + x;
+    int q[16 + BH - 1];
+#pragma unroll
+    for (int i = 0; i < 16 + BH - 1; i++) q[i] = (y0 + i < PREP_R) ? sq127(c[i * PREP_W]) : 0;
+    int s = 0;
+#pragma unroll
+    for (int i = 0; i < BH; i++) s += q[i];
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      vs[(y0 + j) * VS_P + x] = s;
+      if (j < 15) s += q[j + BH] - q[j];
+    }
+  }
+  __syncthreads();
+  const int y = tid >> 2, xs = 16 * (tid & 3);
+  const int yy = r0 + y;
+  if (yy < g.rows_alloc && yy >= row_lo && x0 + xs < g.pitch) {
+    const int4* v4 = reinterpret_cast<const int4*>(vs + y * VS_P + xs);
+    int v[32];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const int4 qq = v4[k];
+      v[4 * k] = qq.x; v[4 * k + 1] = qq.y; v[4 * k + 2] = qq.z; v[4 * k + 3] = qq.w;
+    }
+    int s = 0;
+#pragma unroll
+    for (int j = 0; j < 16; j++) s += v[j];
+    const bool yok = yy <= g.rp_rows - BH;
+    int o[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      o[j] = (yok && x0 + xs + j <= W - 16) ? s : 0;
+      s += v[j + 16] - v[j];
+    }
+    int4* dst = reinterpret_cast<int4*>(plane + (ptrdiff_t)yy * g.pitch + x0 + xs);
+#pragma unroll
+    for (int k = 0; k < 4; k++) dst[k] = make_int4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
+  }
+}
+
+__global__ __launch_bounds__(256) void me_ssd_prep_kernel(SearchArgs p, MfmaGeom g) {
+  __shared__ __align__(16) uint8_t win[PREP_R * PREP_W];
+  __shared__ __align__(16) int vs[64 * VS_P];
+  const int tid = (int)threadIdx.x;
+  // blockIdx.y < nmain: rp and s2 rows [64 y, +64); past it: s2h rows from s2h_row0
+  const int nmain = (g.rows_alloc + 63) / 64;
+  const bool hpass = (int)blockIdx.y >= nmain;
+  const int x0 = (int)blockIdx.x * 64;
+  const int r0 = hpass ? g.s2h_row0 + 64 * ((int)blockIdx.y - nmain) : 64 * (int)blockIdx.y;
+  const int W = p.width;
+  const uint8_t* src = p.ref + (ptrdiff_t)(g.ya0 - p.ref_row0) * p.stride;
+  PS_STAMP(0);
+  // stage; out-of-frame bytes = 127 (square term 0; they only feed zeroed outputs)
+  for (int i = tid; i < PREP_R * (PREP_W / 4); i += 256) {
+    const int rr = i / (PREP_W / 4), cw = i - rr * (PREP_W / 4);
+    const int y = r0 + rr, x = x0 + 4 * cw;
+    uint32_t v = 0x7F7F7F7Fu;
+    if (y < g.rp_rows) {
+      const uint8_t* row = src + (ptrdiff_t)y * p.stride;
+      if (x + 3 < W) {
+        v = *reinterpret_cast<const uint32_t*>(row + x);
+      } else {
+#pragma unroll
+        for (int b = 0; b < 4; b++)
+          if (x + b < W) v = (v & ~(0xFFu << (8 * b))) | ((uint32_t)row[x + b] << (8 * b));
+      }
+    }
+    reinterpret_cast<uint32_t*>(win)[i] = v;
+  }
+  __syncthreads();
+  PS_STAMP(1);
+#if ME_MFMA_ABLATE & 8  // diagnostic: prepass staging only
+  if (win[tid] == 0x5A && tid == 999) g.rp[0] = 1;
+  return;
+#endif
+  if (hpass) {  // hb-row sums for the partial bottom block row's lanes
+    switch (g.hb) {
+#define ME_HB(k) case k: box_pass<k>(g, win, vs, g.s2h, x0, r0, g.s2h_row0, W); break;
+      ME_HB(1) ME_HB(2) ME_HB(3) ME_HB(4) ME_HB(5) ME_HB(6) ME_HB(7) ME_HB(8)
+      ME_HB(9) ME_HB(10) ME_HB(11) ME_HB(12) ME_HB(13) ME_HB(14) ME_HB(15)
+#undef ME_HB
+      default: break;
+    }
+    return;
+  }
+  // rp: 64 x 64 bytes, one dword per thread per round
+  for (int i = tid; i < 64 * 16; i += 256) {
+    const int rr = i >> 4, cw = i & 15;
+    const int y = r0 + rr, x = x0 + 4 * cw;
+    if (y < g.rows_alloc && x < g.pitch) {
+      uint32_t v = reinterpret_cast<const uint32_t*>(win)[rr * (PREP_W / 4) + cw] ^ 0x80808080u;
+      if (y >= g.rp_rows) v = 0;
+      *reinterpret_cast<uint32_t*>(g.rp + (ptrdiff_t)y * g.pitch + x) = v;
+    }
+  }
+#if ME_MFMA_ABLATE & 16  // diagnostic: prepass staging + rp only
+  return;
+#endif
+  PS_STAMP(2);
+  box_pass<16>(g, win, vs, g.s2, x0, r0, 0, W);
+  PS_STAMP(3);
+}
+
+// LDS DMA with 16-byte granules from any byte offset (unaligned sources probed
+// exact on gfx950: tools/mfma_probe.hip); bytes is a multiple of 16.
+template <typename F>
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, uint8_t* lds_dst, int bytes,
+                                      F src_off) {
+  const int tid = opaque((int)threadIdx.x);
+  const int lane = tid & 63, wave = tid >> 6, nw = (int)blockDim.x >> 6;
+  for (int s0 = wave * 1024; s0 < bytes; s0 += nw * 1024) {
+    const int d = s0 + 16 * lane;
+    if (d < bytes)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rs, (__attribute__((address_space(3))) void*)(lds_dst + s0), 16, src_off(d), 0, 0, 0);
+  }
+}
+
+#if ME_MFMA_ABLATE & 64  // diagnostic: no MFMA (one VALU op instead)
+#define MFMA16(A, B, C, x, y, z) ((C) + ((A) ^ (B)))
+#else
+#define MFMA16 __builtin_amdgcn_mfma_i32_16x16x64_i8
+#endif
+
+__device__ __forceinline__ uint32_t sad_u32(uint32_t a_sgpr, uint32_t b, uint32_t c) {
+  uint32_t d;
+  asm("v_sad_u32 %0, %1, %2, %3" : "=v"(d) : "s"(a_sgpr), "v"(b), "v"(c));
+  return d;
+}
+__device__ __forceinline__ uint32_t lshl6_add(uint32_t a, uint32_t b_sgpr) {
+  uint32_t d;
+  asm("v_lshl_add_u32 %0, %1, 6, %2" : "=v"(d) : "v"(a), "s"(b_sgpr));
+  return d;
+}
+
+// ------------------------------------------------------------------ main
+// One workgroup per 4x4 block tile; 4 * NGX waves, wave w = x-subtile
+// (group w >> 2 of 64 positions, phase s = w & 3).  The tile's candidate rows
+// are walked in chunks of L = 13 + 16 * KM rows; per chunk the window rows
+// [y0, y0 + L + 15) are staged as four shifted copies.  Step t of a chunk
+// reads fragment F(t) (window row t + h) -- issued one step ahead -- and runs
+// the MFMAs of output rows t - 4q; the epilogue of row t - 13 follows (its
+// last MFMA ran one step earlier).
+template <int NGX, int KM>
+__global__ __launch_bounds__(256 * NGX)
+__attribute__((amdgpu_waves_per_eu(NGX <= 2 ? 4 : 2))) void me_mfma_ssd16_kernel(SearchArgs p, MfmaGeom g) {
+  constexpr int WP = 64 * NGX + 32;  // bytes per copy row
+  constexpr int L = 13 + 16 * KM;    // candidate rows per chunk
+  constexpr int CROWS = L + 15;
+  constexpr int COPY = CROWS * WP;
+  extern __shared__ __align__(16) uint8_t smem[];
+  unsigned long long* keys = reinterpret_cast<unsigned long long*>(smem + 4 * COPY);
+  int* cc = reinterpret_cast<int*>(smem + 4 * COPY + 16 * 8);
+
+  const int tid = (int)threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n = lane & 15, h = lane >> 4;
+  const int S = p.range, W = p.width, H = p.height;
+  const int tile = (int)blockIdx.x;
+  const int tx = tile % g.tiles_x, ty = tile / g.tiles_x;
+  const int bc0 = 4 * tx, br0 = g.row0 + 4 * ty;
+  const int nbc = min(4, g.nbx - bc0), nbr = min(4, g.row0 + g.nrows - br0);
+  const int tlx0 = 16 * bc0, tly0 = 16 * br0;
+  // block heights: 16, or hb for the frame's partial bottom block row
+  auto bh_of = [&](int br) { return br == g.hb_row ? g.hb : 16; };
+  const int xa = max(tlx0 - S, 0), xb = min(tlx0 + 16 * (nbc - 1) + S, W - 16);
+  const int ya = max(tly0 - S, 0);
+  const int yb = min(tly0 + 16 * (nbr - 1) + S, H - bh_of(br0 + nbr - 1));
+  const int ngx = (xb - xa + 1 + 63) >> 6;
+  const int nch = (yb - ya + 1 + L - 1) / L;
+  const int X0 = xa & ~3;
+
+  const __amdgpu_buffer_rsrc_t rrp =
+      __builtin_amdgcn_make_buffer_rsrc((void*)g.rp, (short)0, g.rp_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs2 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)g.s2, (short)0, g.s2_bytes, 0x00020000);
+
+  auto stage = [&](int y0) {
+    const int base = (y0 - g.ya0) * g.pitch + X0;
+    sfor<0, 4>([&](auto SG) {
+      constexpr int sg = decltype(SG)::value;
+      dma16(rrp, smem + sg * COPY, COPY, [&](int d) {
+        const int rho = d / WP, k = d - rho * WP;
+        return (uint32_t)(base + rho * g.pitch + sg + k);
+      });
+    });
+  };
+
+  MS_STAMP(0, __builtin_amdgcn_s_memtime());
+  MS_STAMP(6, __builtin_amdgcn_s_memrealtime());
+  if (tid < 16) {
+    keys[tid] = ~0ull;
+    cc[tid] = 0;
+  }
+  stage(ya);
+  __syncthreads();
+
+  // A fragments: lane (n, h) holds block n's rows 4q + h as c'' = c ^ 0x7F
+  // (rows past the block height: 0, so they add nothing to X or Cc).
+  v4i a[4];
+  {
+    const int br = n >> 2, bc = n & 3;
+    const bool present = br < nbr && bc < nbc;
+    const int bh = bh_of(br0 + br);
+    int part = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      v4i v = {0, 0, 0, 0};
+      if (present && 4 * q + h < bh) {
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(
+            p.cur + (ptrdiff_t)(tly0 + 16 * br + 4 * q + h - p.cur_row0) * p.stride + tlx0 + 16 * bc);
+#pragma unroll
+        for (int e = 0; e < 4; e++) v[e] = (int)(src[e] ^ 0x7F7F7F7Fu);
+      }
+      a[q] = v;
+#pragma unroll
+      for (int e = 0; e < 4; e++) {
+        part = __builtin_amdgcn_sdot4(v[e], v[e], part, false);
+        part = __builtin_amdgcn_sdot4(v[e], 0x02020202, part, false);
+      }
+    }
+    if (wave == 0 && present) atomicAdd(&cc[n], part);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  MS_STAMP(1, __builtin_amdgcn_s_memtime());
+
+  // Per lane: block row h (y validity, S2 plane), block columns r = 0..3
+  // (x validity through the accumulator start value).
+  uint32_t sumLH, Cv, s2_voff;
+  const int gx = wave >> 2, s = wave & 3;
+  const int xn = xa + 64 * gx + 4 * n + s;
+  {
+    const int tly = tly0 + 16 * h;
+    const int bh = bh_of(br0 + h);
+    int lo = max(tly - S, 0), hi = min(tly + S, H - bh);
+    if (h >= nbr) { lo = 1; hi = 0; }
+    sumLH = (uint32_t)(lo + hi);
+    Cv = 0x80000000u - (uint32_t)(hi - lo) - 1u;
+    s2_voff = (uint32_t)xn * 4u + (bh < 16 ? g.s2h_off : 0u);
+  }
+  const int u = xn - X0, sig = u & 3, ccol = u - sig;
+  v4i initv;
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const int tlx = tlx0 + 16 * r;
+    const int dx = xn - tlx;
+    const bool ok = r < nbc && dx >= max(-S, -tlx) && dx <= min(S, W - 16 - tlx);
+    const int c = cc[4 * h + r];
+    initv[r] = ok ? (c >> 1) : (c >> 1) + (1 << 23);
+  }
+  const bool active = gx < ngx;
+  const uint32_t lds_lane = (uint32_t)(uintptr_t)(
+      (__attribute__((address_space(3))) uint8_t*)smem) + (uint32_t)(sig * COPY + h * WP + ccol);
+
+  for (int ch = 0; ch < nch; ch++) {
+    const int y0 = ya + ch * L;
+    if (ch > 0) {
+      __syncthreads();  // every wave done with the previous chunk's copies
+      if (ch == 1) MS_STAMP(2, __builtin_amdgcn_s_memtime());
+#if !(ME_MFMA_ABLATE & 4)  // diagnostic: stage the first chunk only
+      stage(y0);
+#endif
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+    if (!active) continue;
+    uint32_t best[4] = {~0u, ~0u, ~0u, ~0u};
+    v4i acc[16];
+    v4i fr[2];
+    int sv[4];
+    uint32_t lp = lds_lane;  // window row 4j of the fragments being loaded (advanced every 4 rows)
+    const int s2row0 = (y0 - g.ya0) * g.pitch * 4;  // bytes, row y0 of the S2 planes
+
+    // F(row): row & 3 is static at every call site; lp moves on at rows = 0 mod 4
+    // (two ds_read2_b32 with constant offsets from one base per 4 rows).
+    auto load_row = [&](v4i& dst, auto ROW) {
+      constexpr int row = decltype(ROW)::value;
+      if constexpr ((row & 3) == 0 && row > 0) {
+        lp += 4 * WP;
+        asm volatile("" : "+v"(lp));
+      }
+#if ME_MFMA_ABLATE & 32  // diagnostic: no fragment loads in the loop
+      dst = a[0] ^ (int)lp;
+#else
+      lds_u32* w = reinterpret_cast<lds_u32*>((uintptr_t)lp + (row & 3) * WP);
+      dst[0] = (int)w[0]; dst[1] = (int)w[1]; dst[2] = (int)w[2]; dst[3] = (int)w[3];
+#endif
+    };
+    auto s2load = [&](int yrel) -> int {
+#if ME_MFMA_ABLATE & 1  // diagnostic: no S2 loads
+      return yrel;
+#else
+      return (int)__builtin_amdgcn_raw_buffer_load_b32(rs2, s2_voff, s2row0 + yrel * g.pitch * 4, 0);
+#endif
+    };
+    auto epi = [&](int yrel, const v4i& av, int s2v) {
+#if ME_MFMA_ABLATE & 2  // diagnostic: epilogue reduced to one min per step
+      best[0] = min(best[0], (uint32_t)(av[0] ^ av[1] ^ av[2] ^ av[3] ^ s2v));
+      return;
+#endif
+      const uint32_t P = lshl6_add((uint32_t)s2v, (uint32_t)(64 + yrel));
+      const uint32_t Wd = sad_u32((uint32_t)(2 * (y0 + yrel)), sumLH, Cv);
+      const uint32_t Pf = (Wd & 0x80000000u) | P;
+      const uint32_t k0 = ((uint32_t)av[0] << 7) + Pf, k1 = ((uint32_t)av[1] << 7) + Pf;
+      const uint32_t k2 = ((uint32_t)av[2] << 7) + Pf, k3 = ((uint32_t)av[3] << 7) + Pf;
+      best[0] = min(best[0], k0);
+      best[1] = min(best[1], k1);
+      best[2] = min(best[2], k2);
+      best[3] = min(best[3], k3);
+    };
+
+    load_row(fr[0], std::integral_constant<int, 0>{});
+    // prologue: steps t = 0..12
+    sfor<0, 13>([&](auto TT) {
+      constexpr int t = decltype(TT)::value;
+      load_row(fr[(t + 1) & 1], std::integral_constant<int, t + 1>{});
+      const v4i f = fr[t & 1];
+      sfor<0, 4>([&](auto QQ) {
+        constexpr int q = decltype(QQ)::value;
+        if constexpr (t - 4 * q >= 0) {
+          constexpr int i = (t - 4 * q) & 15;
+          acc[i] = MFMA16(a[q], f, q == 0 ? initv : acc[i], 0, 0, 0);
+        }
+      });
+      if constexpr (t >= 9) sv[(t - 9) & 3] = s2load(t - 9);
+    });
+    // main: t = 13 + 16k + i, every MFMA and the epilogue of y = t - 13
+    for (int k = 0; k < KM; k++) {
+      sfor<0, 16>([&](auto II) {
+        constexpr int i = decltype(II)::value;
+        constexpr int t = 13 + i;  // mod 16
+        const int yrel = 16 * k + i;
+        load_row(fr[(t + 1) & 1], std::integral_constant<int, t + 1>{});
+        const v4i f = fr[t & 1];
+        sfor<0, 4>([&](auto QQ) {
+          constexpr int q = decltype(QQ)::value;
+          constexpr int j = (t - 4 * q) & 15;
+          acc[j] = MFMA16(a[q], f, q == 0 ? initv : acc[j], 0, 0, 0);
+        });
+        epi(yrel, acc[i], sv[i & 3]);
+        sv[i & 3] = s2load(yrel + 4);
+      });
+    }
+    // tail: t = L + e, e = 0..12
+    sfor<0, 13>([&](auto EE) {
+      constexpr int e = decltype(EE)::value;
+      constexpr int t = 13 + e;  // mod 16
+      const int yrel = 16 * KM + e;
+      if constexpr (e < 12) {
+        if constexpr (e < 11) load_row(fr[(t + 1) & 1], std::integral_constant<int, t + 1>{});
+        const v4i f = fr[t & 1];
+        sfor<0, 4>([&](auto QQ) {
+          constexpr int q = decltype(QQ)::value;
+          if constexpr (e < 4 * q) {
+            constexpr int j = (t - 4 * q) & 15;
+            acc[j] = MFMA16(a[q], f, acc[j], 0, 0, 0);
+          }
+        });
+      }
+      epi(yrel, acc[e], sv[e & 3]);
+      if constexpr (e < 9) sv[e & 3] = s2load(yrel + 4);
+    });
+
+    // lane bests -> (cost, dy, dx) keys of the tile's blocks
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const uint32_t b = best[r];
+      if (b < (1u << 30)) {
+        const int m = 4 * h + r;
+        const uint32_t cost = (b >> 6) - 1u + (uint32_t)(cc[m] & 1);
+        const int dy = y0 + (int)(b & 63u) - (tly0 + 16 * h);
+        const int dx = xn - (tlx0 + 16 * r);
+        const unsigned long long key = ((unsigned long long)cost << 32) |
+                                       ((uint32_t)(dy + 32768) << 16) | (uint32_t)(dx + 32768);
+        atomicMin(&keys[m], key);
+      }
+    }
+  }
+  __syncthreads();
+#ifdef ME_STAMPS
+  if (tid == 0 && blockIdx.x < (1u << 14)) {
+    unsigned hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    g_mstamps[8 * blockIdx.x + 3] = __builtin_amdgcn_s_memtime();
+    g_mstamps[8 * blockIdx.x + 4] = hw;
+    g_mstamps[8 * blockIdx.x + 5] = xcc;
+    g_mstamps[8 * blockIdx.x + 7] = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
+  if (tid < 16) {
+    const int br = tid >> 2, bc = tid & 3;
+    if (br < nbr && bc < nbc) {
+      const unsigned long long kk = keys[tid];
+      const int out = (br0 + br - p.block_row_begin) * p.nbx + bc0 + bc;
+      p.mv[2 * out] = (int16_t)((int)(kk & 0xFFFF) - 32768);
+      p.mv[2 * out + 1] = (int16_t)((int)((kk >> 16) & 0xFFFF) - 32768);
+      if (p.cost) p.cost[out] = (uint32_t)(kk >> 32);
+    }
+  }
+}
+
+}  // namespace
+
+// Process-wide path switch (me_set_kernel_path): A/B tests and diagnostics.
+static int g_force_valu = -1;
+void set_force_valu(int v) { g_force_valu = v; }
+bool mfma_disabled() {
+  if (g_force_valu < 0) {
+    const char* e = getenv("ME_PATH");
+    g_force_valu = (e && e[0] == 'v') ? 1 : 0;  // ME_PATH=valu
+  }
+  return g_force_valu == 1;
+}
+
+// Scratch bytes the MFMA path needs for this search (0: path not applicable).
+size_t mfma_ssd_scratch(const SearchArgs& p) {
+  MfmaGeom g;
+  return plan_mfma_ssd(p, &g) ? g.scratch_bytes : 0;
+}
+
+// Full-height block rows [row0, row0 + nrows) and full-width columns of a B = 16
+// SSD search; the caller routes partial rows / columns to the VALU kernels.
+bool plan_mfma_ssd(const SearchArgs& p, MfmaGeom* g) {
+  if (p.cost_kind != COST_SSD || p.blk != 16) return false;
+  if (mfma_disabled()) return false;
+  const int S = p.range, W = p.width, H = p.height;
+  if (S < 1 || W < 16 || H < 16) return false;
+  if (p.stride % 4 || (uintptr_t)p.cur % 4 || (uintptr_t)p.ref % 4) return false;
+  const int nxmax = min(48 + 2 * S + 1, W - 15);
+  const int ngx = (nxmax + 63) / 64;
+  if (ngx > 4) return false;  // S > 103: the VALU kernels take it
+  const int nby = (H + 15) / 16;
+  const int r0 = p.block_row_begin, r1 = p.block_row_end;
+  g->row0 = r0;
+  g->nrows = r1 - r0;
+  if (g->nrows <= 0) return false;
+  // partial bottom block row (height hb): its lanes read the hb-row S2 plane
+  g->hb = H - 16 * (nby - 1);
+  g->hb_row = (g->hb < 16 && r1 == nby) ? nby - 1 : -1;
+  if (g->hb_row < 0) g->hb = 16;
+  g->nbx = W / 16;
+  g->tiles_x = (g->nbx + 3) / 4;
+  g->tiles_y = (g->nrows + 3) / 4;
+  g->ngx = ngx;
+  // chunk rows L = 13 + 16 KM: fewest (chunks x (L + 13)) steps on an interior tile
+  const int ny = min(48 + 2 * S + 1, H - 15);
+  int best = 1 << 30;
+  for (int km = 2; km <= 3; km++) {  // km = 1 spills (its lone main-loop pass gets peeled)
+    const int L = 13 + 16 * km, ch = (ny + L - 1) / L;
+    const int cost = ch * (L + 13);
+    if (cost < best) { best = cost; g->km = km; }
+  }
+  const int L = 13 + 16 * g->km;
+  g->lds = 4 * (L + 15) * (64 * ngx + 32) + 16 * 8 + 16 * 4;
+  g->ya0 = max(r0 * 16 - S, 0);
+  const int ya1 = min(r1 * 16 + S, H);
+  g->rp_rows = ya1 - g->ya0;
+  g->pitch = (W + 15) & ~15;
+  // + 80 rows of slack: the last chunk of a tile reads (masked) window rows and
+  // S2 entries up to L + 15 rows past the planes' last row.
+  g->rows_alloc = g->rp_rows + 80;
+  // the last tile row's candidate rows start here (its lanes of the partial
+  // block row read s2h from there on)
+  const int tly_last = 16 * (r0 + 4 * (g->tiles_y - 1));
+  g->s2h_row0 = max(tly_last - S, 0) - g->ya0;
+  const size_t plane = (size_t)g->rows_alloc * g->pitch;
+  const size_t rp_alloc = (plane + 255) & ~(size_t)255;
+  const size_t s2_plane = plane * 4;
+  const size_t n_s2 = g->hb < 16 ? 2 : 1;
+  if (rp_alloc + n_s2 * s2_plane >= (1ull << 31)) return false;
+  g->rp_bytes = (uint32_t)plane;
+  g->s2_bytes = (uint32_t)(n_s2 * s2_plane);
+  g->s2h_off = (uint32_t)s2_plane;
+  g->scratch_bytes = rp_alloc + n_s2 * s2_plane;
+  g->rp = reinterpret_cast<int8_t*>(p.scratch);
+  g->s2 = p.scratch ? reinterpret_cast<int*>(p.scratch + rp_alloc) : nullptr;
+  g->s2h = p.scratch ? reinterpret_cast<int*>(p.scratch + rp_alloc + s2_plane) : nullptr;
+  return true;
+}
+
+hipError_t launch_mfma_ssd(const SearchArgs& p, const MfmaGeom& g, hipStream_t stream) {
+  const int nmain = (g.rows_alloc + 63) / 64;
+  const int nh = g.hb < 16 ? (g.rows_alloc - g.s2h_row0 + 63) / 64 : 0;
+  dim3 pgrid((unsigned)((g.pitch + 63) / 64), (unsigned)(nmain + nh));
+  hipLaunchKernelGGL(me_ssd_prep_kernel, pgrid, dim3(256), 0, stream, p, g);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const dim3 grid((unsigned)(g.tiles_x * g.tiles_y));
+#define ME_MFMA_CASE(NG, KK)                                                              \
+  if (g.ngx == NG && g.km == KK) {                                                        \
+    const void* fn = (const void*)me_mfma_ssd16_kernel<NG, KK>;                           \
+    if (g.lds > 64 * 1024) {                                                              \
+      e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, g.lds);     \
+      if (e != hipSuccess) return e;                                                      \
+    }                                                                                     \
+    hipLaunchKernelGGL((me_mfma_ssd16_kernel<NG, KK>), grid, dim3(256 * NG), g.lds, stream, p, g); \
+    return hipGetLastError();                                                             \
+  }
+  ME_MFMA_CASE(1, 2) ME_MFMA_CASE(1, 3)
+  ME_MFMA_CASE(2, 2) ME_MFMA_CASE(2, 3)
+  ME_MFMA_CASE(3, 2) ME_MFMA_CASE(3, 3)
+  ME_MFMA_CASE(4, 2) ME_MFMA_CASE(4, 3)
+#undef ME_MFMA_CASE
+  return hipErrorInvalidValue;
+}
+
+}  // namespace me
+
+#ifdef ME_STAMPS
+extern "C" int me_debug_prep_stamps(unsigned long long* out, int n_words) {
+  if (n_words > (6 << 14)) n_words = 6 << 14;
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(me::g_pstamps), (size_t)n_words * 8, 0,
+                                  hipMemcpyDeviceToHost);
+}
+extern "C" int me_debug_mfma_stamps(unsigned long long* out, int n_words) {
+  if (n_words > (8 << 14)) n_words = 8 << 14;
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(me::g_mstamps), (size_t)n_words * 8, 0,
+                                  hipMemcpyDeviceToHost);
+}
+#endif

@@ -202,7 +202,10 @@ me_status run_pairs(me_ctx* c, Dev& d, const Job& j, int p0, int p1) {
     const size_t o = (size_t)(n - p0) * nb;
     me::SearchArgs p = make_args(d.slots[sr], 0, d.slots[sc], 0, W, H, W, B, j.range, j.cost, 0,
                                  nby, out_mv + 2 * o, out_cost + o);
-    p.sched = d.sched;
+    {
+      const me_status st = me::attach_scratch(c, d, p);
+      if (st != ME_OK) return st;
+    }
     HIPCHK(c, me::launch_search(p, d.stream, nullptr));
     for (int side = 0; side < 2; side++) {
       const int f = j.pairs[2 * n + side];

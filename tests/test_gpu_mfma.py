@@ -1,0 +1,122 @@
+"""Matrix-core SSD path (me_mfma.hip: i8 MFMA cross term + S2 prepass) against
+the oracle and against the VALU kernels, bit-exact (MVs and integer SSDs).
+
+The MFMA path serves B = 16 SSD on full blocks; tiles of 4x4 blocks, chunks of
+L = 45/61 candidate rows, 1-4 groups of 64 candidate columns (S up to 103).
+The cases cover every (groups, chunk length) instance, frame edges on all four
+sides, tiles with missing block rows / columns, partial right columns and
+bottom rows (handed to the VALU kernels), stride != width, stripes whose ref
+plane holds only the halo rows, and the extreme key ranges (SSD 0 and the
+largest SSD 256 * 255^2)."""
+import os
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+import motionestimation_amd as me
+from motionestimation_amd import synth
+
+pytestmark = pytest.mark.gpu
+NT = min(16, os.cpu_count() or 1)
+
+
+def _pair(rng, h, w, dx=2, dy=-1, noise=3):
+    ref = synth._box5(rng.integers(0, 256, (h, w), dtype=np.uint8))
+    cur = np.clip(synth.shift_plane(ref, dx, dy).astype(int) + rng.integers(-noise, noise + 1, (h, w)),
+                  0, 255).astype(np.uint8)
+    return ref, cur
+
+
+def _check(engine, ref, cur, span, tag, stride=None):
+    mv, cost = engine.full_search(ref, cur, 16, span, "ssd", stride=stride)
+    omv, ocost, _ = O.full_search(ref, cur, 16, span, "ssd", threads=NT)
+    np.testing.assert_array_equal(mv, omv, err_msg=tag)
+    np.testing.assert_array_equal(cost, ocost, err_msg=tag)
+
+
+@pytest.mark.parametrize("span", [1, 2, 3, 7, 8, 13, 16, 17, 24, 31, 32, 40, 47, 48, 63, 64, 80, 103])
+def test_mfma_ssd_spans(engine, span):
+    """Every (64-column groups, chunk length) instance the planner picks, with
+    frame edges on all sides and tiles that lack block rows or columns."""
+    rng = np.random.default_rng(1000 + span)
+    for (h, w) in [(96, 128), (150, 200), (64, 352)]:
+        ref, cur = _pair(rng, h, w, dx=(span % 5) - 2, dy=2 - (span % 3))
+        _check(engine, ref, cur, span, f"{h}x{w} S{span}")
+
+
+def test_mfma_vs_valu_path(engine):
+    """Same search on both kernel paths: identical outputs."""
+    rng = np.random.default_rng(7)
+    try:
+        for (h, w, span) in [(288, 352, 16), (200, 320, 32), (176, 240, 64), (120, 176, 7)]:
+            ref, cur = _pair(rng, h, w, dx=3, dy=-3)
+            me.set_kernel_path("auto")
+            a = engine.full_search(ref, cur, 16, span, "ssd")
+            me.set_kernel_path("valu")
+            b = engine.full_search(ref, cur, 16, span, "ssd")
+            np.testing.assert_array_equal(a[0], b[0], err_msg=f"{h}x{w} S{span}")
+            np.testing.assert_array_equal(a[1], b[1])
+    finally:
+        me.set_kernel_path("auto")
+
+
+def test_mfma_extreme_values(engine):
+    """Key range ends: SSD 0 everywhere (all ties), the largest SSD (0 vs 255),
+    and mixed saturated planes."""
+    h, w = 80, 112
+    zeros, full = np.zeros((h, w), np.uint8), np.full((h, w), 255, np.uint8)
+    rng = np.random.default_rng(3)
+    noise = rng.integers(0, 256, (h, w), dtype=np.uint8)
+    binary = (rng.integers(0, 2, (h, w)) * 255).astype(np.uint8)
+    for tag, ref, cur in [("flat", full, full), ("zeros", zeros, zeros), ("max", zeros, full),
+                          ("max2", full, zeros), ("noise/0", noise, zeros), ("0/noise", zeros, noise),
+                          ("binary", binary, np.roll(binary, 3, axis=1)), ("noise", noise, noise)]:
+        for span in (5, 32):
+            _check(engine, ref, cur, span, f"{tag} S{span}")
+
+
+def test_mfma_partial_edges_and_stride(engine):
+    """Partial right column / bottom row (VALU kernels beside the MFMA tiles)
+    and a row pitch larger than the width."""
+    rng = np.random.default_rng(11)
+    for (h, w, span) in [(100, 150, 16), (73, 201, 9), (40, 36, 32), (17, 17, 4), (16, 16, 8)]:
+        ref, cur = _pair(rng, h, w)
+        _check(engine, ref, cur, span, f"{h}x{w} S{span}")
+    import torch
+    ref, cur = _pair(rng, 96, 160)
+    pad_r = np.zeros((96, 200), np.uint8)
+    pad_c = np.zeros((96, 200), np.uint8)
+    pad_r[:, :160], pad_c[:, :160] = ref, cur
+    rt, ct = torch.from_numpy(pad_r).cuda(), torch.from_numpy(pad_c).cuda()
+    n = me.num_blocks(160, 96, 16)
+    mvt = torch.empty((n, 2), dtype=torch.int16, device="cuda")
+    cot = torch.empty(n, dtype=torch.int32, device="cuda")
+    engine.full_search_device(rt, ct, 16, 20, "ssd", mvt, cot, width=160, height=96, stride=200)
+    torch.cuda.synchronize()
+    omv, ocost, _ = O.full_search(ref, cur, 16, 20, "ssd", threads=NT)
+    np.testing.assert_array_equal(mvt.cpu().numpy(), omv)
+    np.testing.assert_array_equal(cot.cpu().numpy().view(np.uint32), ocost)
+
+
+def test_mfma_stripes_halo_only(engine):
+    """Row stripes whose ref plane holds only [r0*B - S, r1*B + S): the
+    prepass and the window DMA see exactly the resident rows."""
+    import torch
+    rng = np.random.default_rng(5)
+    h, w, blk, span = 208, 256, 16, 24
+    ref, cur = _pair(rng, h, w, dx=-3, dy=4)
+    omv, ocost, _ = O.full_search(ref, cur, blk, span, "ssd", threads=NT)
+    nbx = w // blk
+    for (r0, r1) in [(0, 3), (3, 7), (7, 13), (5, 6)]:
+        y0, y1 = max(0, r0 * blk - span), min(h, r1 * blk + span)
+        rt = torch.from_numpy(np.ascontiguousarray(ref[y0:y1])).cuda()
+        ct = torch.from_numpy(np.ascontiguousarray(cur[r0 * blk:r1 * blk])).cuda()
+        n = (r1 - r0) * nbx
+        mvt = torch.empty((n, 2), dtype=torch.int16, device="cuda")
+        cot = torch.empty(n, dtype=torch.int32, device="cuda")
+        engine.search_stripe_device(rt, y0, ct, r0 * blk, w, h, blk, span, "ssd", r0, r1, mvt, cot)
+        torch.cuda.synchronize()
+        sl = slice(r0 * nbx, r1 * nbx)
+        np.testing.assert_array_equal(mvt.cpu().numpy(), omv[sl], err_msg=f"rows {r0}-{r1}")
+        np.testing.assert_array_equal(cot.cpu().numpy().view(np.uint32), ocost[sl])
