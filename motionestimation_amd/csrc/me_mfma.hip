@@ -43,6 +43,9 @@
 
 #include "me_kernels.h"
 
+#ifndef ME_MFMA_DLY
+#define ME_MFMA_DLY 1  // 1..3 (the 16-register accumulator ring holds 13 + DLY rows)
+#endif
 #ifndef ME_MFMA_ABLATE
 #define ME_MFMA_ABLATE 0  // diagnostic bit set (csrc/Makefile mablate, tools/mablate.sh); never shipped
 #endif
@@ -150,7 +153,13 @@ __device__ __forceinline__ void box_pass(const MfmaGeom& g, const uint8_t* win, 
     }
     int4* dst = reinterpret_cast<int4*>(plane + (ptrdiff_t)yy * g.pitch + x0 + xs);
 #pragma unroll
-    for (int k = 0; k < 4; k++) dst[k] = make_int4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
+    for (int k = 0; k < 4; k++) {
+      // non-temporal: the planes are read by the next kernel, not this one;
+      // nothing dirty is left in L2 for the end-of-kernel write-back
+      typedef int i32x4 __attribute__((ext_vector_type(4)));
+      const i32x4 v = {o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]};
+      __builtin_nontemporal_store(v, reinterpret_cast<i32x4*>(dst) + k);
+    }
   }
 }
 
@@ -206,7 +215,7 @@ __global__ __launch_bounds__(256) void me_ssd_prep_kernel(SearchArgs p, MfmaGeom
     if (y < g.rows_alloc && x < g.pitch) {
       uint32_t v = reinterpret_cast<const uint32_t*>(win)[rr * (PREP_W / 4) + cw] ^ 0x80808080u;
       if (y >= g.rp_rows) v = 0;
-      *reinterpret_cast<uint32_t*>(g.rp + (ptrdiff_t)y * g.pitch + x) = v;
+      __builtin_nontemporal_store(v, reinterpret_cast<uint32_t*>(g.rp + (ptrdiff_t)y * g.pitch + x));
     }
   }
 #if ME_MFMA_ABLATE & 16  // diagnostic: prepass staging + rp only
@@ -261,12 +270,16 @@ template <int NGX, int KM>
 __global__ __launch_bounds__(256 * NGX)
 __attribute__((amdgpu_waves_per_eu(NGX <= 2 ? 4 : 2))) void me_mfma_ssd16_kernel(SearchArgs p, MfmaGeom g) {
   constexpr int WP = 64 * NGX + 32;  // bytes per copy row
-  constexpr int L = 13 + 16 * KM;    // candidate rows per chunk
+  constexpr int DLY = ME_MFMA_DLY;      // steps between a row's last MFMA and its epilogue
+  constexpr int P0 = 12 + DLY;         // prologue steps (= epilogue lag)
+  constexpr int L = P0 + 16 * KM;      // candidate rows per chunk
   constexpr int CROWS = L + 15;
   constexpr int COPY = CROWS * WP;
   extern __shared__ __align__(16) uint8_t smem[];
+  constexpr int RB = 256 * NGX;        // bytes per S2 table row (64 NGX positions)
   unsigned long long* keys = reinterpret_cast<unsigned long long*>(smem + 4 * COPY);
   int* cc = reinterpret_cast<int*>(smem + 4 * COPY + 16 * 8);
+  uint8_t* s2t = smem + 4 * COPY + 16 * 8 + 16 * 4;  // S2 of the chunk: [L][64 NGX] ints
 
   const int tid = (int)threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n = lane & 15, h = lane >> 4;
@@ -282,7 +295,11 @@ __attribute__((amdgpu_waves_per_eu(NGX <= 2 ? 4 : 2))) void me_mfma_ssd16_kernel
   const int ya = max(tly0 - S, 0);
   const int yb = min(tly0 + 16 * (nbr - 1) + S, H - bh_of(br0 + nbr - 1));
   const int ngx = (xb - xa + 1 + 63) >> 6;
-  const int nch = (yb - ya + 1 + L - 1) / L;
+  // tiles holding the frame's partial bottom block row read S2 from global
+  // memory (see chunk()); they walk shorter chunks (L - 16) to finish with the rest
+  const bool tile_hb = g.hb_row >= br0 && g.hb_row < br0 + nbr;
+  const int Lt = (tile_hb && KM > 2) ? L - 16 : L;
+  const int nch = (yb - ya + 1 + Lt - 1) / Lt;
   const int X0 = xa & ~3;
 
   const __amdgpu_buffer_rsrc_t rrp =
@@ -294,10 +311,17 @@ __attribute__((amdgpu_waves_per_eu(NGX <= 2 ? 4 : 2))) void me_mfma_ssd16_kernel
     const int base = (y0 - g.ya0) * g.pitch + X0;
     sfor<0, 4>([&](auto SG) {
       constexpr int sg = decltype(SG)::value;
-      dma16(rrp, smem + sg * COPY, COPY, [&](int d) {
+      dma16(rrp, smem + sg * COPY, (Lt + 15) * WP, [&](int d) {
         const int rho = d / WP, k = d - rho * WP;
         return (uint32_t)(base + rho * g.pitch + sg + k);
       });
+    });
+    // S2 rows [y0, y0 + L) x positions [xa, xa + 64 NGX) of the 16-row plane
+    if (tile_hb) return;
+    const int sbase = ((y0 - g.ya0) * g.pitch + xa) * 4;
+    dma16(rs2, s2t, L * RB, [&](int d) {
+      const int rho = d / RB, k = d - rho * RB;
+      return (uint32_t)(sbase + rho * g.pitch * 4 + k);
     });
   };
 
@@ -367,9 +391,11 @@ __attribute__((amdgpu_waves_per_eu(NGX <= 2 ? 4 : 2))) void me_mfma_ssd16_kernel
   const bool active = gx < ngx;
   const uint32_t lds_lane = (uint32_t)(uintptr_t)(
       (__attribute__((address_space(3))) uint8_t*)smem) + (uint32_t)(sig * COPY + h * WP + ccol);
+  const uint32_t s2t_lane = (uint32_t)(uintptr_t)(
+      (__attribute__((address_space(3))) uint8_t*)s2t) + (uint32_t)(64 * gx + 4 * n + s) * 4u;
 
   for (int ch = 0; ch < nch; ch++) {
-    const int y0 = ya + ch * L;
+    const int y0 = ya + ch * Lt;
     if (ch > 0) {
       __syncthreads();  // every wave done with the previous chunk's copies
       if (ch == 1) MS_STAMP(2, __builtin_amdgcn_s_memtime());
@@ -379,7 +405,8 @@ __attribute__((amdgpu_waves_per_eu(NGX <= 2 ? 4 : 2))) void me_mfma_ssd16_kernel
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
-    if (!active) continue;
+    auto chunk = [&](auto HBC) {
+      constexpr int KMc = (decltype(HBC)::value && KM > 2) ? KM - 1 : KM;  // = (Lt - P0) / 16
     uint32_t best[4] = {~0u, ~0u, ~0u, ~0u};
     v4i acc[16];
     v4i fr[2];
@@ -402,11 +429,20 @@ __attribute__((amdgpu_waves_per_eu(NGX <= 2 ? 4 : 2))) void me_mfma_ssd16_kernel
       dst[0] = (int)w[0]; dst[1] = (int)w[1]; dst[2] = (int)w[2]; dst[3] = (int)w[3];
 #endif
     };
-    auto s2load = [&](int yrel) -> int {
+    uint32_t sp = s2t_lane;  // S2 table row 16k of the main loop
+    auto s2load = [&](int yrel_static_off, int yrel) -> int {
 #if ME_MFMA_ABLATE & 1  // diagnostic: no S2 loads
       return yrel;
 #else
-      return (int)__builtin_amdgcn_raw_buffer_load_b32(rs2, s2_voff, s2row0 + yrel * g.pitch * 4, 0);
+      if constexpr (decltype(HBC)::value) {
+        // the lanes' S2 planes differ (s2 / s2h): straight from global memory
+        (void)yrel_static_off;
+        return (int)__builtin_amdgcn_raw_buffer_load_b32(rs2, s2_voff, s2row0 + yrel * g.pitch * 4, 0);
+      } else {
+        typedef __attribute__((address_space(3))) const int lds_i32;
+        (void)yrel;
+        return *reinterpret_cast<lds_i32*>((uintptr_t)(sp + (uint32_t)yrel_static_off * RB));
+      }
 #endif
     };
     auto epi = [&](int yrel, const v4i& av, int s2v) {
@@ -426,8 +462,8 @@ __attribute__((amdgpu_waves_per_eu(NGX <= 2 ? 4 : 2))) void me_mfma_ssd16_kernel
     };
 
     load_row(fr[0], std::integral_constant<int, 0>{});
-    // prologue: steps t = 0..12
-    sfor<0, 13>([&](auto TT) {
+    // prologue: steps t = 0 .. P0-1
+    sfor<0, P0>([&](auto TT) {
       constexpr int t = decltype(TT)::value;
       load_row(fr[(t + 1) & 1], std::integral_constant<int, t + 1>{});
       const v4i f = fr[t & 1];
@@ -438,13 +474,14 @@ __attribute__((amdgpu_waves_per_eu(NGX <= 2 ? 4 : 2))) void me_mfma_ssd16_kernel
           acc[i] = MFMA16(a[q], f, q == 0 ? initv : acc[i], 0, 0, 0);
         }
       });
-      if constexpr (t >= 9) sv[(t - 9) & 3] = s2load(t - 9);
+      if constexpr (t >= P0 - 4) sv[(t - P0 + 4) & 3] = s2load(t - P0 + 4, t - P0 + 4);
     });
-    // main: t = 13 + 16k + i, every MFMA and the epilogue of y = t - 13
-    for (int k = 0; k < KM; k++) {
+    // main: t = P0 + 16k + i, every MFMA and the epilogue of y = t - P0
+    // (its last MFMA ran DLY steps earlier)
+    for (int k = 0; k < KMc; k++) {
       sfor<0, 16>([&](auto II) {
         constexpr int i = decltype(II)::value;
-        constexpr int t = 13 + i;  // mod 16
+        constexpr int t = P0 + i;  // mod 16
         const int yrel = 16 * k + i;
         load_row(fr[(t + 1) & 1], std::integral_constant<int, t + 1>{});
         const v4i f = fr[t & 1];
@@ -454,14 +491,16 @@ __attribute__((amdgpu_waves_per_eu(NGX <= 2 ? 4 : 2))) void me_mfma_ssd16_kernel
           acc[j] = MFMA16(a[q], f, q == 0 ? initv : acc[j], 0, 0, 0);
         });
         epi(yrel, acc[i], sv[i & 3]);
-        sv[i & 3] = s2load(yrel + 4);
+        sv[i & 3] = s2load(i + 4, yrel + 4);
       });
+      sp += 16 * RB;
+      asm volatile("" : "+v"(sp));
     }
-    // tail: t = L + e, e = 0..12
-    sfor<0, 13>([&](auto EE) {
+    // tail: t = L + e, e = 0 .. P0-1
+    sfor<0, P0>([&](auto EE) {
       constexpr int e = decltype(EE)::value;
-      constexpr int t = 13 + e;  // mod 16
-      const int yrel = 16 * KM + e;
+      constexpr int t = P0 + e;  // mod 16
+      const int yrel = 16 * KMc + e;
       if constexpr (e < 12) {
         if constexpr (e < 11) load_row(fr[(t + 1) & 1], std::integral_constant<int, t + 1>{});
         const v4i f = fr[t & 1];
@@ -474,7 +513,7 @@ __attribute__((amdgpu_waves_per_eu(NGX <= 2 ? 4 : 2))) void me_mfma_ssd16_kernel
         });
       }
       epi(yrel, acc[e], sv[e & 3]);
-      if constexpr (e < 9) sv[e & 3] = s2load(yrel + 4);
+      if constexpr (e < P0 - 4) sv[e & 3] = s2load(e + 4, yrel + 4);
     });
 
     // lane bests -> (cost, dy, dx) keys of the tile's blocks
@@ -490,6 +529,11 @@ __attribute__((amdgpu_waves_per_eu(NGX <= 2 ? 4 : 2))) void me_mfma_ssd16_kernel
                                        ((uint32_t)(dy + 32768) << 16) | (uint32_t)(dx + 32768);
         atomicMin(&keys[m], key);
       }
+    }
+    };
+    if (active) {
+      if (tile_hb) chunk(std::true_type{});
+      else chunk(std::false_type{});
     }
   }
   __syncthreads();
@@ -559,16 +603,16 @@ bool plan_mfma_ssd(const SearchArgs& p, MfmaGeom* g) {
   g->tiles_x = (g->nbx + 3) / 4;
   g->tiles_y = (g->nrows + 3) / 4;
   g->ngx = ngx;
-  // chunk rows L = 13 + 16 KM: fewest (chunks x (L + 13)) steps on an interior tile
+  // chunk rows L = P0 + 16 KM: fewest (chunks x (L + P0)) steps on an interior tile
   const int ny = min(48 + 2 * S + 1, H - 15);
   int best = 1 << 30;
   for (int km = 2; km <= 3; km++) {  // km = 1 spills (its lone main-loop pass gets peeled)
-    const int L = 13 + 16 * km, ch = (ny + L - 1) / L;
-    const int cost = ch * (L + 13);
+    const int L = 12 + ME_MFMA_DLY + 16 * km, ch = (ny + L - 1) / L;
+    const int cost = ch * (L + 12 + ME_MFMA_DLY);
     if (cost < best) { best = cost; g->km = km; }
   }
-  const int L = 13 + 16 * g->km;
-  g->lds = 4 * (L + 15) * (64 * ngx + 32) + 16 * 8 + 16 * 4;
+  const int L = 12 + ME_MFMA_DLY + 16 * g->km;
+  g->lds = 4 * (L + 15) * (64 * ngx + 32) + 16 * 8 + 16 * 4 + L * 256 * ngx;
   g->ya0 = max(r0 * 16 - S, 0);
   const int ya1 = min(r1 * 16 + S, H);
   g->rp_rows = ya1 - g->ya0;

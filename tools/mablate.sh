@@ -11,7 +11,7 @@ out=$R/gpurun_out/mablate.txt
 mkdir -p gpurun_out
 : > $out
 export TMPDIR=/tmp
-for lib in libme_hip.so $(cd motionestimation_amd/lib && ls libme_hip_mabl*.so); do
+for lib in libme_hip.so $(cd motionestimation_amd/lib && ls libme_hip_mabl*.so libme_hip_mdly*.so); do
   d=$R/gpurun_out/mabl_$lib
   (cd /tmp && ME_HIP_LIB=$lib timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $d -o run --output-format csv -- python3 $R/tools/size_sweep.py --cost ssd --heights 1080 --iters 50 > $d.log 2>&1)
   echo "== $lib" >> $out

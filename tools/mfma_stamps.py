@@ -72,3 +72,8 @@ print(f"prepass: {len(full)} main workgroups; cycles median: stage {np.median(fu
 ra, rb = full[:, 4] - full[:, 4].min(), full[:, 5] - full[:, 4].min()
 print(f"prepass realtime us: starts min {ra.min()/100:.2f} median {np.median(ra)/100:.2f} max {ra.max()/100:.2f}; "
       f"ends max {rb.max()/100:.2f}")
+# slowest workgroups (tile index = blockIdx.x for the MFMA kernel)
+ids = np.nonzero(buf.reshape(-1, 8)[:, 3] > 0)[0]
+life = b - a
+order = np.argsort(-life)[:12]
+print("  slowest WGs (blockIdx, lifetime us):", [(int(ids[i]), round(float(life[i]), 1)) for i in order])
