@@ -37,6 +37,7 @@ sys.path.insert(0, REPO)
 METRIC = "16×16 SAD candidates/sec at 1080p ±32; achieved HBM GB/s vs roofline"
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
 VALU_PEAK_ABSDIFF = 157.3e12  # 256 CU x 64 lanes x 2.4 GHz x 4 |a-b| per op (measured: profiles/)
+I8_PEAK_TOPS = 5000.0         # MI355X_MICROARCH.md: dense I8 MFMA = 2x BF16 (2.5 PF) per clock
 CONFIGS = {  # name -> (synth config, block, range)
     "1080p": ("1080p", 16, 32),
     "4k": ("4k", 16, 64),
@@ -53,6 +54,8 @@ def parse():
     ap.add_argument("--config", choices=list(CONFIGS), default="1080p")
     ap.add_argument("--cost", choices=["sad", "ssd", "ssim"], default="sad")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-ssd", action="store_true",
+                    help="skip the SSD (matrix-core) line beside a SAD run")
     ap.add_argument("--no-stream", action="store_true",
                     help="skip the host frame-pair streaming leg (PCIe-inclusive, not `value`)")
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -149,6 +152,29 @@ def host_stream(eng, w, h, blk, span, cost, seed, sx, sy, kern_ms, cands_frame):
     out["kernel_only_pairs_per_s"] = 1e3 / kern_ms
     del pinned
     return out
+
+
+def ssd_beside(eng, ref_t, cur_t, blk, span, nb, cands_frame, dev, steps):
+    """The reference's own cost (MSE = SSD / 256) on the same resident frame pair:
+    B = 16 SSD runs on the matrix cores (i8 MFMA).  Reported beside `value`."""
+    import torch
+    mv = torch.empty((nb, 2), dtype=torch.int16, device=dev)
+    co = torch.empty(nb, dtype=torch.int32, device=dev)
+    for _ in range(3):
+        eng.full_search_device(ref_t, cur_t, blk, span, "ssd", mv, co)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(steps):
+        eng.full_search_device(ref_t, cur_t, blk, span, "ssd", mv, co)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / steps
+    tops = 2.0 * blk * blk * cands_frame / (ms / 1e3) / 1e12
+    return {"value": cands_frame / (ms / 1e3), "unit": "candidates/s", "kernel_ms": ms,
+            "steps": steps, "cost": "ssd (reference MSE argmin, bit-exact)",
+            "roofline": {"bound": "mfma", "achieved": tops, "peak": I8_PEAK_TOPS,
+                         "unit": "TFLOP/s", "frac": tops / I8_PEAK_TOPS}}
 
 
 def load_traffic(tag):
@@ -310,6 +336,23 @@ def main():
     }
     if args.cost == "ssim":  # float chains, not abs-diffs: no VALU-peak claim
         line["roofline"]["valu"] = None
+    if args.cost == "ssd" and blk == 16:
+        # B = 16 SSD runs on the matrix cores (i8 MFMA cross term): the bound is
+        # the MFMA peak; algorithmic ops = 2 x 256 multiply-adds per candidate
+        ops = 2.0 * blk * blk * (cands_frame if args.mode == "frames" else cands_frame / world)
+        tops = ops / (kern_ms / 1e3) / 1e12
+        hbm = line["roofline"]
+        hbm.pop("valu", None)
+        line["roofline"] = {"bound": "mfma", "achieved": tops, "peak": I8_PEAK_TOPS,
+                            "unit": "TFLOP/s", "frac": tops / I8_PEAK_TOPS, "traffic": traffic,
+                            "note": "useful int8 ops (2*256 per candidate) over the whole search "
+                                    "(S2 prepass + MFMA kernel); dense i8 peak",
+                            "hbm": {k: hbm[k] for k in ("achieved", "peak", "unit", "frac",
+                                                        "algorithmic_bytes_per_launch")}}
+    if (rank == 0 and world == 1 and args.mode == "frames" and args.cost == "sad"
+            and blk == 16 and not args.no_ssd):
+        line["ssd_mfma"] = ssd_beside(eng, ref_t, cur_t, blk, span, nb, cands_frame, dev,
+                                      min(args.steps, 20))
     if parity is not None:
         line["stripe_gather_parity"] = parity
     if rank == 0 and world == 1 and not args.no_cpu:

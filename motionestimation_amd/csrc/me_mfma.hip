@@ -284,7 +284,15 @@ __attribute__((amdgpu_waves_per_eu(NGX <= 2 ? 4 : 2))) void me_mfma_ssd16_kernel
   const int tid = (int)threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n = lane & 15, h = lane >> 4;
   const int S = p.range, W = p.width, H = p.height;
-  const int tile = (int)blockIdx.x;
+  // XCD-aware tile order: workgroups are dealt round-robin over the 8 XCDs
+  // (bid % 8, a speed heuristic only), so XCD x gets one contiguous band of
+  // tiles and its L2 holds that band's window and S2 rows.
+  int tile;
+  {
+    const int nwg = (int)gridDim.x, bid = (int)blockIdx.x;
+    const int x = bid & 7, m = bid >> 3, q = nwg >> 3, rem = nwg & 7;
+    tile = x * q + min(x, rem) + m;
+  }
   const int tx = tile % g.tiles_x, ty = tile / g.tiles_x;
   const int bc0 = 4 * tx, br0 = g.row0 + 4 * ty;
   const int nbc = min(4, g.nbx - bc0), nbr = min(4, g.row0 + g.nrows - br0);
