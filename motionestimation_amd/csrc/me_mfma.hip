@@ -19,9 +19,9 @@
 // the tiles y = R, R-4, R-8, R-12 (q = 0..3): one 16-byte LDS fragment per
 // four MFMAs.  Positions of a wave are x_n = xbase + 4n + s (stride 4): all
 // its lanes share the byte alignment of x_n, and the window is held in LDS as
-// four copies shifted by 0..3 bytes (LDS DMA from unaligned offsets, probed
-// exact on gfx950: tools/mfma_probe.hip), so every fragment read is dword
-// aligned and needs no realignment.
+// four copies shifted by 0..3 bytes (copy 0 by LDS DMA, copies 1..3 built
+// from it with v_alignbyte), so every fragment read is dword aligned and the
+// loop needs no realignment.
 //
 // Epilogue per output tile, per lane (position n, block row h, block column r
 // in result register r): 32-bit keys
@@ -315,14 +315,13 @@ __attribute__((amdgpu_waves_per_eu(NGX <= 2 ? 4 : 2))) void me_mfma_ssd16_kernel
   const __amdgpu_buffer_rsrc_t rs2 =
       __builtin_amdgcn_make_buffer_rsrc((void*)g.s2, (short)0, g.s2_bytes, 0x00020000);
 
+  // Copy 0 of the window arrives by LDS DMA; copies 1..3 (shifted by 1..3
+  // bytes) are built from it in LDS (v_alignbyte), not fetched again.
   auto stage = [&](int y0) {
     const int base = (y0 - g.ya0) * g.pitch + X0;
-    sfor<0, 4>([&](auto SG) {
-      constexpr int sg = decltype(SG)::value;
-      dma16(rrp, smem + sg * COPY, (Lt + 15) * WP, [&](int d) {
-        const int rho = d / WP, k = d - rho * WP;
-        return (uint32_t)(base + rho * g.pitch + sg + k);
-      });
+    dma16(rrp, smem, (Lt + 15) * WP, [&](int d) {
+      const int rho = d / WP, k = d - rho * WP;
+      return (uint32_t)(base + rho * g.pitch + k);
     });
     // S2 rows [y0, y0 + L) x positions [xa, xa + 64 NGX) of the 16-row plane
     if (tile_hb) return;
@@ -331,6 +330,27 @@ __attribute__((amdgpu_waves_per_eu(NGX <= 2 ? 4 : 2))) void me_mfma_ssd16_kernel
       const int rho = d / RB, k = d - rho * RB;
       return (uint32_t)(sbase + rho * g.pitch * 4 + k);
     });
+  };
+
+  auto shift_copies = [&]() {
+    typedef __attribute__((address_space(3))) uint32_t lds_w32;
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(3))) u32x4 lds_w128;
+    constexpr int QW = WP / 16;  // 16-byte groups per row
+    const int nq = (Lt + 15) * QW;
+    for (int i = opaque(tid); i < nq; i += (int)blockDim.x) {
+      const int rho = i / QW, c = i - rho * QW;
+      const uint32_t off = (uint32_t)(rho * WP + 16 * c);
+      const uint32_t lbase = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) uint8_t*)smem);
+      const u32x4 w = *reinterpret_cast<lds_w128*>((uintptr_t)(lbase + off));
+      const uint32_t nx = c + 1 < QW ? *reinterpret_cast<lds_w32*>((uintptr_t)(lbase + off + 16)) : 0u;
+      sfor<1, 4>([&](auto SG) {
+        constexpr int sg = decltype(SG)::value;
+        const u32x4 o = {__builtin_amdgcn_alignbyte(w[1], w[0], sg), __builtin_amdgcn_alignbyte(w[2], w[1], sg),
+                         __builtin_amdgcn_alignbyte(w[3], w[2], sg), __builtin_amdgcn_alignbyte(nx, w[3], sg)};
+        *reinterpret_cast<lds_w128*>((uintptr_t)(lbase + sg * COPY + off)) = o;
+      });
+    }
   };
 
   MS_STAMP(0, __builtin_amdgcn_s_memtime());
@@ -370,6 +390,8 @@ __attribute__((amdgpu_waves_per_eu(NGX <= 2 ? 4 : 2))) void me_mfma_ssd16_kernel
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  shift_copies();
+  __syncthreads();
   MS_STAMP(1, __builtin_amdgcn_s_memtime());
 
   // Per lane: block row h (y validity, S2 plane), block columns r = 0..3
@@ -397,8 +419,13 @@ __attribute__((amdgpu_waves_per_eu(NGX <= 2 ? 4 : 2))) void me_mfma_ssd16_kernel
     initv[r] = ok ? (c >> 1) : (c >> 1) + (1 << 23);
   }
   const bool active = gx < ngx;
+#if ME_MFMA_ABLATE & 128  // diagnostic: every lane group reads the same row (no bank conflicts)
+  const uint32_t lds_lane = (uint32_t)(uintptr_t)(
+      (__attribute__((address_space(3))) uint8_t*)smem) + (uint32_t)(sig * COPY + ccol);
+#else
   const uint32_t lds_lane = (uint32_t)(uintptr_t)(
       (__attribute__((address_space(3))) uint8_t*)smem) + (uint32_t)(sig * COPY + h * WP + ccol);
+#endif
   const uint32_t s2t_lane = (uint32_t)(uintptr_t)(
       (__attribute__((address_space(3))) uint8_t*)s2t) + (uint32_t)(64 * gx + 4 * n + s) * 4u;
 
@@ -411,6 +438,8 @@ __attribute__((amdgpu_waves_per_eu(NGX <= 2 ? 4 : 2))) void me_mfma_ssd16_kernel
       stage(y0);
 #endif
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      shift_copies();
       __syncthreads();
     }
     auto chunk = [&](auto HBC) {
