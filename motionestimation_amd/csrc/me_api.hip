@@ -90,11 +90,33 @@ SearchArgs make_args(const uint8_t* ref, int ref_row0, const uint8_t* cur, int c
   p.sched = nullptr;
   p.scratch = nullptr;
   p.scratch_bytes = 0;
+  p.mkeys = nullptr;
+  p.mcnt = nullptr;
+  p.merge_tiles = 0;
   return p;
 }
 
 me_status attach_scratch(me_ctx* c, Dev& d, SearchArgs& p) {
   p.sched = d.sched;
+  if (p.cost_kind == COST_SSD) {
+    const size_t tiles = mfma_merge_tiles(p);
+    if (tiles > d.merge_cap) {
+      (void)hipFree(d.mkeys);
+      (void)hipFree(d.mcnt);
+      d.mkeys = nullptr;
+      d.mcnt = nullptr;
+      d.merge_cap = 0;
+      if (hipMalloc((void**)&d.mkeys, tiles * 16 * 8) != hipSuccess ||
+          hipMalloc((void**)&d.mcnt, tiles * 4) != hipSuccess ||
+          hipMemset(d.mkeys, 0xFF, tiles * 16 * 8) != hipSuccess ||
+          hipMemset(d.mcnt, 0, tiles * 4) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+        return fail(c, ME_ENOMEM, "MFMA merge buffers (%zu tiles)", tiles);
+      d.merge_cap = tiles;
+    }
+  }
+  p.mkeys = d.mkeys;
+  p.mcnt = d.mcnt;
+  p.merge_tiles = d.merge_cap;
   const size_t need = mfma_ssd_scratch(p);
   if (need) {
     me_status s = grow(c, (void**)&d.scratch, &d.scratch_cap, need);
@@ -347,6 +369,8 @@ void me_destroy(me_ctx* c) {
     (void)hipFree(d.out5);
     (void)hipFree(d.sched);
     (void)hipFree(d.scratch);
+    (void)hipFree(d.mkeys);
+    (void)hipFree(d.mcnt);
     me::release_pipeline(d);
     if (d.stream) (void)hipStreamDestroy(d.stream);
   }

@@ -31,6 +31,9 @@ struct Dev {
   uint32_t* sched = nullptr;  // fast-kernel tile counters (self-resetting)
   uint8_t* scratch = nullptr; // MFMA SSD prepass planes (me_mfma.hip), grown on demand
   size_t scratch_cap = 0;
+  unsigned long long* mkeys = nullptr;  // MFMA SSD merge keys (~0) and tile counters (0):
+  uint32_t* mcnt = nullptr;             //   initialised on allocation, self-resetting after
+  size_t merge_cap = 0;                 //   (tiles)
   // Frame-pair pipeline (me_stream.hip), kept across calls.
   std::vector<uint8_t*> slots;        // device frames, slot_bytes each
   std::vector<hipEvent_t> slot_ready; // upload of the slot's frame done (copy stream)

@@ -31,6 +31,11 @@ struct SearchArgs {
   uint32_t* sched;     // 9 zeroed u32 (8 XCD-group tile counters + arrivals) or null
   uint8_t* scratch;    // device scratch of the MFMA SSD path (mfma_ssd_scratch bytes) or null
   size_t scratch_bytes;
+  // MFMA SSD cross-workgroup merge (self-resetting): 16 keys (~0) per tile and
+  // one arrival counter (0) per tile, merge_tiles tiles; or null
+  unsigned long long* mkeys;
+  uint32_t* mcnt;
+  size_t merge_tiles;
 };
 
 struct QsadGeom {
@@ -60,7 +65,8 @@ struct QsadGeom {
 struct MfmaGeom {
   int row0, nrows, nbx;
   int tiles_x, tiles_y;
-  int ngx;               // 64-position groups per tile row of candidates (waves = 4 ngx)
+  int ngx;               // 64-position groups per tile
+  int ngxw;              // groups per workgroup (1 or 2; 4 waves each)
   int km;                // candidate rows per chunk L = 13 + 16 km
   int lds;               // dynamic LDS bytes
   int hb, hb_row;        // partial bottom block row: height hb, block row index (-1: none)
@@ -74,7 +80,10 @@ struct MfmaGeom {
   int8_t* rp;            // ref ^ 0x80
   int* s2;               // 16x16 box sums of (ref - 127)^2
   int* s2h;              // hb x 16 box sums (partial bottom row only)
+  unsigned long long* mkeys;  // per tile 16 merge keys (~0 between launches)
+  uint32_t* mcnt;        // per tile arrival counters (0 between launches)
 };
+size_t mfma_merge_tiles(const SearchArgs& p);  // tiles the merge buffers must cover
 bool plan_mfma_ssd(const SearchArgs& p, MfmaGeom* g);
 hipError_t launch_mfma_ssd(const SearchArgs& p, const MfmaGeom& g, hipStream_t stream);
 size_t mfma_ssd_scratch(const SearchArgs& p);  // 0: path not applicable

@@ -268,7 +268,8 @@ __device__ __forceinline__ uint32_t lshl6_add(uint32_t a, uint32_t b_sgpr) {
 // last MFMA ran one step earlier).
 template <int NGX, int KM>
 __global__ __launch_bounds__(256 * NGX)
-__attribute__((amdgpu_waves_per_eu(NGX <= 2 ? 4 : 2))) void me_mfma_ssd16_kernel(SearchArgs p, MfmaGeom g) {
+__attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd16_kernel(SearchArgs p, MfmaGeom g) {
+  // NGX 64-position groups per workgroup (4 waves each)
   constexpr int WP = 64 * NGX + 32;  // bytes per copy row
   constexpr int DLY = ME_MFMA_DLY;      // steps between a row's last MFMA and its epilogue
   constexpr int P0 = 12 + DLY;         // prologue steps (= epilogue lag)
@@ -287,11 +288,16 @@ __attribute__((amdgpu_waves_per_eu(NGX <= 2 ? 4 : 2))) void me_mfma_ssd16_kernel
   // XCD-aware tile order: workgroups are dealt round-robin over the 8 XCDs
   // (bid % 8, a speed heuristic only), so XCD x gets one contiguous band of
   // tiles and its L2 holds that band's window and S2 rows.
-  int tile;
+  // Workgroup = (tile, wg-th run of NGX groups of 64 candidate columns); a
+  // tile's workgroups are adjacent in this order, so they share an XCD band.
+  const int wpt = (g.ngx + NGX - 1) / NGX;  // workgroups per tile (launch-wide)
+  int tile, wg;
   {
     const int nwg = (int)gridDim.x, bid = (int)blockIdx.x;
     const int x = bid & 7, m = bid >> 3, q = nwg >> 3, rem = nwg & 7;
-    tile = x * q + min(x, rem) + m;
+    const int lin = x * q + min(x, rem) + m;
+    tile = lin / wpt;
+    wg = lin - tile * wpt;
   }
   const int tx = tile % g.tiles_x, ty = tile / g.tiles_x;
   const int bc0 = 4 * tx, br0 = g.row0 + 4 * ty;
@@ -302,13 +308,16 @@ __attribute__((amdgpu_waves_per_eu(NGX <= 2 ? 4 : 2))) void me_mfma_ssd16_kernel
   const int xa = max(tlx0 - S, 0), xb = min(tlx0 + 16 * (nbc - 1) + S, W - 16);
   const int ya = max(tly0 - S, 0);
   const int yb = min(tly0 + 16 * (nbr - 1) + S, H - bh_of(br0 + nbr - 1));
-  const int ngx = (xb - xa + 1 + 63) >> 6;
+  const int ngx = (xb - xa + 1 + 63) >> 6;  // groups this tile needs (<= g.ngx)
+  const int nwt = (ngx + NGX - 1) / NGX;     // workgroups this tile needs
+  if (wg >= nwt) return;  // uniform; the tile's arrival count is nwt
+  const int gx0 = wg * NGX;                  // first group of this workgroup
   // tiles holding the frame's partial bottom block row read S2 from global
   // memory (see chunk()); they walk shorter chunks (L - 16) to finish with the rest
   const bool tile_hb = g.hb_row >= br0 && g.hb_row < br0 + nbr;
   const int Lt = (tile_hb && KM > 2) ? L - 16 : L;
   const int nch = (yb - ya + 1 + Lt - 1) / Lt;
-  const int X0 = xa & ~3;
+  const int X0 = (xa + 64 * gx0) & ~3;  // window column origin of this workgroup
 
   const __amdgpu_buffer_rsrc_t rrp =
       __builtin_amdgcn_make_buffer_rsrc((void*)g.rp, (short)0, g.rp_bytes, 0x00020000);
@@ -323,9 +332,9 @@ __attribute__((amdgpu_waves_per_eu(NGX <= 2 ? 4 : 2))) void me_mfma_ssd16_kernel
       const int rho = d / WP, k = d - rho * WP;
       return (uint32_t)(base + rho * g.pitch + k);
     });
-    // S2 rows [y0, y0 + L) x positions [xa, xa + 64 NGX) of the 16-row plane
+    // S2 rows [y0, y0 + L) x this workgroup's positions [xa + 64 gx0, +64 NGX) (16-row plane)
     if (tile_hb) return;
-    const int sbase = ((y0 - g.ya0) * g.pitch + xa) * 4;
+    const int sbase = ((y0 - g.ya0) * g.pitch + xa + 64 * gx0) * 4;
     dma16(rs2, s2t, L * RB, [&](int d) {
       const int rho = d / RB, k = d - rho * RB;
       return (uint32_t)(sbase + rho * g.pitch * 4 + k);
@@ -397,7 +406,7 @@ __attribute__((amdgpu_waves_per_eu(NGX <= 2 ? 4 : 2))) void me_mfma_ssd16_kernel
   // Per lane: block row h (y validity, S2 plane), block columns r = 0..3
   // (x validity through the accumulator start value).
   uint32_t sumLH, Cv, s2_voff;
-  const int gx = wave >> 2, s = wave & 3;
+  const int gx = gx0 + (wave >> 2), s = wave & 3;  // positions x_n = xa + 64 gx + 4n + s
   const int xn = xa + 64 * gx + 4 * n + s;
   {
     const int tly = tly0 + 16 * h;
@@ -418,7 +427,6 @@ __attribute__((amdgpu_waves_per_eu(NGX <= 2 ? 4 : 2))) void me_mfma_ssd16_kernel
     const int c = cc[4 * h + r];
     initv[r] = ok ? (c >> 1) : (c >> 1) + (1 << 23);
   }
-  const bool active = gx < ngx;
 #if ME_MFMA_ABLATE & 128  // diagnostic: every lane group reads the same row (no bank conflicts)
   const uint32_t lds_lane = (uint32_t)(uintptr_t)(
       (__attribute__((address_space(3))) uint8_t*)smem) + (uint32_t)(sig * COPY + ccol);
@@ -427,7 +435,8 @@ __attribute__((amdgpu_waves_per_eu(NGX <= 2 ? 4 : 2))) void me_mfma_ssd16_kernel
       (__attribute__((address_space(3))) uint8_t*)smem) + (uint32_t)(sig * COPY + h * WP + ccol);
 #endif
   const uint32_t s2t_lane = (uint32_t)(uintptr_t)(
-      (__attribute__((address_space(3))) uint8_t*)s2t) + (uint32_t)(64 * gx + 4 * n + s) * 4u;
+      (__attribute__((address_space(3))) uint8_t*)s2t) + (uint32_t)(64 * (gx - gx0) + 4 * n + s) * 4u;
+  const bool active = gx < ngx;
 
   for (int ch = 0; ch < nch; ch++) {
     const int y0 = ya + ch * Lt;
@@ -585,16 +594,45 @@ __attribute__((amdgpu_waves_per_eu(NGX <= 2 ? 4 : 2))) void me_mfma_ssd16_kernel
     g_mstamps[8 * blockIdx.x + 7] = __builtin_amdgcn_s_memrealtime();
   }
 #endif
-  if (tid < 16) {
-    const int br = tid >> 2, bc = tid & 3;
-    if (br < nbr && bc < nbc) {
-      const unsigned long long kk = keys[tid];
-      const int out = (br0 + br - p.block_row_begin) * p.nbx + bc0 + bc;
-      p.mv[2 * out] = (int16_t)((int)(kk & 0xFFFF) - 32768);
-      p.mv[2 * out + 1] = (int16_t)((int)((kk >> 16) & 0xFFFF) - 32768);
-      if (p.cost) p.cost[out] = (uint32_t)(kk >> 32);
+  // Merge the tile's groups: with one group the keys are final; otherwise each
+  // group folds its keys into the tile's global keys (device-scope atomicMin)
+  // and the last group to arrive writes the outputs and resets the keys and
+  // its counter for the next launch (self-resetting scratch, me_internal.h).
+  const int br = tid >> 2, bc = tid & 3;
+  const bool outb = tid < 16 && br < nbr && bc < nbc;
+  unsigned long long* gk = g.mkeys + 16 * (size_t)tile + tid;
+  // Only atomics carry data between the groups (all at the device coherence
+  // point), so completion order is enough: each group waits for its returning
+  // atomicMins before its arrival increment; no fences (a device-scope release
+  // writes back L2).
+  bool last = nwt == 1;
+  if (!last) {
+    int* flag = reinterpret_cast<int*>(keys + 16);  // scratch word past the keys
+    if (outb) {
+      const unsigned long long old = __hip_atomic_fetch_min(gk, keys[tid], __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" : : "v"((uint32_t)old) : "memory");
     }
+    __syncthreads();
+    if (tid == 0) {
+      const unsigned arrived = __hip_atomic_fetch_add(g.mcnt + tile, 1u, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT);
+      flag[0] = arrived == (unsigned)nwt - 1u;
+    }
+    __syncthreads();
+    last = flag[0] != 0;
   }
+  if (last && outb) {
+    const unsigned long long kk =
+        nwt == 1 ? keys[tid]
+                 : __hip_atomic_exchange(gk, ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int out = (br0 + br - p.block_row_begin) * p.nbx + bc0 + bc;
+    p.mv[2 * out] = (int16_t)((int)(kk & 0xFFFF) - 32768);
+    p.mv[2 * out + 1] = (int16_t)((int)((kk >> 16) & 0xFFFF) - 32768);
+    if (p.cost) p.cost[out] = (uint32_t)(kk >> 32);
+  }
+  if (last && nwt > 1 && tid == 0)
+    __hip_atomic_store(g.mcnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 }  // namespace
@@ -608,6 +646,14 @@ bool mfma_disabled() {
     g_force_valu = (e && e[0] == 'v') ? 1 : 0;  // ME_PATH=valu
   }
   return g_force_valu == 1;
+}
+
+// Tiles of a B = 16 search over block rows [begin, end) (the merge buffers' size).
+size_t mfma_merge_tiles(const SearchArgs& p) {
+  if (p.blk != 16 || p.width < 16) return 0;
+  const size_t tx = (size_t)((p.width / 16 + 3) / 4);
+  const size_t ty = (size_t)((p.block_row_end - p.block_row_begin + 3) / 4);
+  return tx * ty;
 }
 
 // Scratch bytes the MFMA path needs for this search (0: path not applicable).
@@ -643,13 +689,35 @@ bool plan_mfma_ssd(const SearchArgs& p, MfmaGeom* g) {
   // chunk rows L = P0 + 16 KM: fewest (chunks x (L + P0)) steps on an interior tile
   const int ny = min(48 + 2 * S + 1, H - 15);
   int best = 1 << 30;
+  static int force_km = -1;  // ME_MFMA_KM=2|3: tuning override, read once
+  if (force_km < 0) {
+    const char* e = getenv("ME_MFMA_KM");
+    force_km = e ? atoi(e) : 0;
+  }
   for (int km = 2; km <= 3; km++) {  // km = 1 spills (its lone main-loop pass gets peeled)
+    if (force_km && km != force_km) continue;
     const int L = 12 + ME_MFMA_DLY + 16 * km, ch = (ny + L - 1) / L;
     const int cost = ch * (L + 12 + ME_MFMA_DLY);
     if (cost < best) { best = cost; g->km = km; }
   }
   const int L = 12 + ME_MFMA_DLY + 16 * g->km;
-  g->lds = 4 * (L + 15) * (64 * ngx + 32) + 16 * 8 + 16 * 4 + L * 256 * ngx;
+  // groups per workgroup: two when the tile needs an even number of groups
+  // (whole tiles at 1080p +-32: no merge), else one (4K +-64: 3 workgroups)
+  g->ngxw = ngx % 2 == 0 ? 2 : 1;
+  {
+    static int force_w = -1;  // ME_MFMA_NGXW=1|2: tuning override, read once
+    if (force_w < 0) {
+      const char* e = getenv("ME_MFMA_NGXW");
+      force_w = e ? atoi(e) : 0;
+    }
+    if (force_w == 1 || force_w == 2) g->ngxw = force_w;
+  }
+  if ((ngx + g->ngxw - 1) / g->ngxw > 1 &&
+      (!p.mkeys || !p.mcnt || p.merge_tiles < mfma_merge_tiles(p)))
+    return false;  // tiles span workgroups: needs the merge buffers
+  g->lds = 4 * (L + 15) * (64 * g->ngxw + 32) + 16 * 8 + 16 * 4 + L * 256 * g->ngxw;
+  g->mkeys = p.mkeys;
+  g->mcnt = p.mcnt;
   g->ya0 = max(r0 * 16 - S, 0);
   const int ya1 = min(r1 * 16 + S, H);
   g->rp_rows = ya1 - g->ya0;
@@ -683,21 +751,19 @@ hipError_t launch_mfma_ssd(const SearchArgs& p, const MfmaGeom& g, hipStream_t s
   hipLaunchKernelGGL(me_ssd_prep_kernel, pgrid, dim3(256), 0, stream, p, g);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  const dim3 grid((unsigned)(g.tiles_x * g.tiles_y));
+  const int wpt = (g.ngx + g.ngxw - 1) / g.ngxw;
+  const dim3 grid((unsigned)(g.tiles_x * g.tiles_y * wpt));
 #define ME_MFMA_CASE(NG, KK)                                                              \
-  if (g.ngx == NG && g.km == KK) {                                                        \
-    const void* fn = (const void*)me_mfma_ssd16_kernel<NG, KK>;                           \
+  if (g.ngxw == NG && g.km == KK) {                                                       \
     if (g.lds > 64 * 1024) {                                                              \
-      e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, g.lds);     \
+      e = hipFuncSetAttribute((const void*)me_mfma_ssd16_kernel<NG, KK>,                  \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, g.lds);         \
       if (e != hipSuccess) return e;                                                      \
     }                                                                                     \
     hipLaunchKernelGGL((me_mfma_ssd16_kernel<NG, KK>), grid, dim3(256 * NG), g.lds, stream, p, g); \
     return hipGetLastError();                                                             \
   }
-  ME_MFMA_CASE(1, 2) ME_MFMA_CASE(1, 3)
-  ME_MFMA_CASE(2, 2) ME_MFMA_CASE(2, 3)
-  ME_MFMA_CASE(3, 2) ME_MFMA_CASE(3, 3)
-  ME_MFMA_CASE(4, 2) ME_MFMA_CASE(4, 3)
+  ME_MFMA_CASE(1, 2) ME_MFMA_CASE(1, 3) ME_MFMA_CASE(2, 2) ME_MFMA_CASE(2, 3)
 #undef ME_MFMA_CASE
   return hipErrorInvalidValue;
 }
