@@ -336,16 +336,16 @@ def main():
     }
     if args.cost == "ssim":  # float chains, not abs-diffs: no VALU-peak claim
         line["roofline"]["valu"] = None
-    if args.cost == "ssd" and blk == 16:
-        # B = 16 SSD runs on the matrix cores (i8 MFMA cross term): the bound is
-        # the MFMA peak; algorithmic ops = 2 x 256 multiply-adds per candidate
+    if args.cost == "ssd" and blk in (8, 16):
+        # B = 8 and 16 SSD run on the matrix cores (i8 MFMA cross term): the bound is
+        # the MFMA peak; algorithmic ops = 2 x B*B multiply-adds per candidate
         ops = 2.0 * blk * blk * (cands_frame if args.mode == "frames" else cands_frame / world)
         tops = ops / (kern_ms / 1e3) / 1e12
         hbm = line["roofline"]
         hbm.pop("valu", None)
         line["roofline"] = {"bound": "mfma", "achieved": tops, "peak": I8_PEAK_TOPS,
                             "unit": "TFLOP/s", "frac": tops / I8_PEAK_TOPS, "traffic": traffic,
-                            "note": "useful int8 ops (2*256 per candidate) over the whole search "
+                            "note": "useful int8 ops (2*B*B per candidate) over the whole search "
                                     "(S2 prepass + MFMA kernel); dense i8 peak",
                             "hbm": {k: hbm[k] for k in ("achieved", "peak", "unit", "frac",
                                                         "algorithmic_bytes_per_launch")}}

@@ -1085,7 +1085,18 @@ hipError_t launch_search(const SearchArgs& p, hipStream_t stream, int* used_fast
     hipError_t e = launch_mfma_ssd(p, mg, stream);
     if (e != hipSuccess) return e;
     if (used_fast) *used_fast = 2;
-    if (mg.nbx < p.nbx) return launch_generic(p, mg.nbx, p.nbx - mg.nbx, r0, r1 - r0, stream);
+    const int rest = mg.row0 + mg.nrows;  // < r1: a partial bottom row the MFMA kernel left (B = 8)
+    if (mg.nbx < p.nbx) {
+      e = launch_generic(p, mg.nbx, p.nbx - mg.nbx, r0, rest - r0, stream);
+      if (e != hipSuccess) return e;
+    }
+    if (rest < r1) {
+      SearchArgs q = p;
+      q.block_row_begin = rest;
+      q.mv = p.mv + 2 * (size_t)(rest - r0) * p.nbx;
+      if (p.cost) q.cost = p.cost + (size_t)(rest - r0) * p.nbx;
+      return launch_valu(q, stream, nullptr);
+    }
     return hipSuccess;
   }
   return launch_valu(p, stream, used_fast);

@@ -110,7 +110,7 @@ __device__ __forceinline__ int sq127(int v) {
 // Vertical BH-row sums of one 16-row segment per task (every byte load
 // independent: one LDS latency per task), then horizontal 16-sums per
 // (row, 16 columns) in registers -> plane rows [row_lo, rows_alloc).
-template <int BH>
+template <int BH, int BW>
 __device__ __forceinline__ void box_pass(const MfmaGeom& g, const uint8_t* win, int* vs, int* plane,
                                          int x0, int r0, int row_lo, int W) {
   const int tid = (int)threadIdx.x;
@@ -143,13 +143,13 @@ __device__ __forceinline__ void box_pass(const MfmaGeom& g, const uint8_t* win, 
     }
     int s = 0;
 #pragma unroll
-    for (int j = 0; j < 16; j++) s += v[j];
+    for (int j = 0; j < BW; j++) s += v[j];
     const bool yok = yy <= g.rp_rows - BH;
     int o[16];
 #pragma unroll
     for (int j = 0; j < 16; j++) {
-      o[j] = (yok && x0 + xs + j <= W - 16) ? s : 0;
-      s += v[j + 16] - v[j];
+      o[j] = (yok && x0 + xs + j <= W - BW) ? s : 0;
+      s += v[j + BW] - v[j];
     }
     int4* dst = reinterpret_cast<int4*>(plane + (ptrdiff_t)yy * g.pitch + x0 + xs);
 #pragma unroll
@@ -163,6 +163,7 @@ __device__ __forceinline__ void box_pass(const MfmaGeom& g, const uint8_t* win, 
   }
 }
 
+template <int B>
 __global__ __launch_bounds__(256) void me_ssd_prep_kernel(SearchArgs p, MfmaGeom g) {
   __shared__ __align__(16) uint8_t win[PREP_R * PREP_W];
   __shared__ __align__(16) int vs[64 * VS_P];
@@ -200,7 +201,7 @@ __global__ __launch_bounds__(256) void me_ssd_prep_kernel(SearchArgs p, MfmaGeom
 #endif
   if (hpass) {  // hb-row sums for the partial bottom block row's lanes
     switch (g.hb) {
-#define ME_HB(k) case k: box_pass<k>(g, win, vs, g.s2h, x0, r0, g.s2h_row0, W); break;
+#define ME_HB(k) case k: if constexpr (k < B) box_pass<k, B>(g, win, vs, g.s2h, x0, r0, g.s2h_row0, W); break;
       ME_HB(1) ME_HB(2) ME_HB(3) ME_HB(4) ME_HB(5) ME_HB(6) ME_HB(7) ME_HB(8)
       ME_HB(9) ME_HB(10) ME_HB(11) ME_HB(12) ME_HB(13) ME_HB(14) ME_HB(15)
 #undef ME_HB
@@ -222,7 +223,7 @@ __global__ __launch_bounds__(256) void me_ssd_prep_kernel(SearchArgs p, MfmaGeom
   return;
 #endif
   PS_STAMP(2);
-  box_pass<16>(g, win, vs, g.s2, x0, r0, 0, W);
+  box_pass<B, B>(g, win, vs, g.s2, x0, r0, 0, W);
   PS_STAMP(3);
 }
 
@@ -635,6 +636,246 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd16_kernel(SearchArgs p, 
     __hip_atomic_store(g.mcnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// ------------------------------------------------------------- 8x8 blocks
+// B = 8: K = 64 is a whole block, so one MFMA finishes an output tile (16
+// positions at one y x the 16 blocks of a 4x4-block tile): lane (n, h) holds
+// block rows 2h, 2h+1 (A) and window rows y + 2h, y + 2h + 1 at x_n (B).  No
+// accumulator ring; per step one fragment (two ds_read2_b32), one MFMA and the
+// same 32-bit key epilogue as the 16x16 kernel:
+//   key = ((S2 + 1) << 6) + (y - y0) + (acc << 7) = (SSD - p + 1) << 6 | (y - y0)
+// SSD <= 64 * 255^2 < 2^22, so valid keys < 2^28; x out of window: acc + 2^22
+// (keys in [2^29, 2^30)); y out of window: bit 31.  Chunks of L = 64 rows.
+// Workgroup = (tile, one group of 64 candidate columns), 4 waves (phase s);
+// tiles spanning several workgroups merge like the 16x16 kernel.
+template <int KM8>
+__global__ __launch_bounds__(256)
+__attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd8_kernel(SearchArgs p, MfmaGeom g) {
+  constexpr int WP = 64 + 32;      // bytes per copy row (64 positions + 7 + align)
+  constexpr int L = 16 * KM8;      // candidate rows per chunk (yidx < 64)
+  constexpr int CROWS = L + 8;     // rows y0 .. y0 + L + 6, + the last (unused) prefetch
+  constexpr int COPY = CROWS * WP;
+  constexpr int RB = 256;          // bytes per S2 table row (L + 1 rows: one prefetch past)
+  static_assert(L <= 64, "6-bit row index");
+  extern __shared__ __align__(16) uint8_t smem[];
+  unsigned long long* keys = reinterpret_cast<unsigned long long*>(smem + 4 * COPY);
+  int* cc = reinterpret_cast<int*>(smem + 4 * COPY + 16 * 8);
+  uint8_t* s2t = smem + 4 * COPY + 16 * 8 + 16 * 4;  // [L][64] ints
+
+  const int tid = (int)threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n = lane & 15, h = lane >> 4;
+  const int S = p.range, W = p.width, H = p.height;
+  const int wpt = g.ngx;  // one group per workgroup
+  int tile, gx;
+  {
+    const int nwg = (int)gridDim.x, bid = (int)blockIdx.x;
+    const int x = bid & 7, m = bid >> 3, q = nwg >> 3, rem = nwg & 7;
+    const int lin = x * q + min(x, rem) + m;
+    tile = lin / wpt;
+    gx = lin - tile * wpt;
+  }
+  const int tx = tile % g.tiles_x, ty = tile / g.tiles_x;
+  const int bc0 = 4 * tx, br0 = g.row0 + 4 * ty;
+  const int nbc = min(4, g.nbx - bc0), nbr = min(4, g.row0 + g.nrows - br0);
+  const int tlx0 = 8 * bc0, tly0 = 8 * br0;
+  const int xa = max(tlx0 - S, 0), xb = min(tlx0 + 8 * (nbc - 1) + S, W - 8);
+  const int ya = max(tly0 - S, 0), yb = min(tly0 + 8 * (nbr - 1) + S, H - 8);
+  const int ngx = (xb - xa + 1 + 63) >> 6;
+  if (gx >= ngx) return;  // uniform; the tile's arrival count is ngx
+  const int nch = (yb - ya + 1 + L - 1) / L;
+  const int X0 = (xa + 64 * gx) & ~3;
+
+  const __amdgpu_buffer_rsrc_t rrp =
+      __builtin_amdgcn_make_buffer_rsrc((void*)g.rp, (short)0, g.rp_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs2 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)g.s2, (short)0, g.s2_bytes, 0x00020000);
+
+  auto stage = [&](int y0) {
+    const int base = (y0 - g.ya0) * g.pitch + X0;
+    dma16(rrp, smem, COPY, [&](int d) {
+      const int rho = d / WP, k = d - rho * WP;
+      return (uint32_t)(base + rho * g.pitch + k);
+    });
+    const int sbase = ((y0 - g.ya0) * g.pitch + xa + 64 * gx) * 4;
+    dma16(rs2, s2t, L * RB, [&](int d) {
+      const int rho = d / RB, k = d - rho * RB;
+      return (uint32_t)(sbase + rho * g.pitch * 4 + k);
+    });
+  };
+  auto shift_copies = [&]() {
+    typedef __attribute__((address_space(3))) uint32_t lds_w32;
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(3))) u32x4 lds_w128;
+    constexpr int QW = WP / 16;
+    const uint32_t lbase = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) uint8_t*)smem);
+    for (int i = opaque(tid); i < CROWS * QW; i += 256) {
+      const int rho = i / QW, c = i - rho * QW;
+      const uint32_t off = (uint32_t)(rho * WP + 16 * c);
+      const u32x4 w = *reinterpret_cast<lds_w128*>((uintptr_t)(lbase + off));
+      const uint32_t nx = c + 1 < QW ? *reinterpret_cast<lds_w32*>((uintptr_t)(lbase + off + 16)) : 0u;
+      sfor<1, 4>([&](auto SG) {
+        constexpr int sg = decltype(SG)::value;
+        const u32x4 o = {__builtin_amdgcn_alignbyte(w[1], w[0], sg), __builtin_amdgcn_alignbyte(w[2], w[1], sg),
+                         __builtin_amdgcn_alignbyte(w[3], w[2], sg), __builtin_amdgcn_alignbyte(nx, w[3], sg)};
+        *reinterpret_cast<lds_w128*>((uintptr_t)(lbase + sg * COPY + off)) = o;
+      });
+    }
+  };
+
+  if (tid < 16) {
+    keys[tid] = ~0ull;
+    cc[tid] = 0;
+  }
+  stage(ya);
+  __syncthreads();
+  // A fragment: lane (n, h) holds block n's rows 2h, 2h+1 as c'' = c ^ 0x7F
+  v4i a;
+  {
+    const int br = n >> 2, bc = n & 3;
+    const bool present = br < nbr && bc < nbc;
+    v4i v = {0, 0, 0, 0};
+    if (present) {
+      const uint8_t* row = p.cur + (ptrdiff_t)(tly0 + 8 * br + 2 * h - p.cur_row0) * p.stride + tlx0 + 8 * bc;
+      const uint32_t* r0 = reinterpret_cast<const uint32_t*>(row);
+      const uint32_t* r1 = reinterpret_cast<const uint32_t*>(row + p.stride);
+      v[0] = (int)(r0[0] ^ 0x7F7F7F7Fu); v[1] = (int)(r0[1] ^ 0x7F7F7F7Fu);
+      v[2] = (int)(r1[0] ^ 0x7F7F7F7Fu); v[3] = (int)(r1[1] ^ 0x7F7F7F7Fu);
+    }
+    a = v;
+    int part = 0;
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+      part = __builtin_amdgcn_sdot4(v[e], v[e], part, false);
+      part = __builtin_amdgcn_sdot4(v[e], 0x02020202, part, false);
+    }
+    if (wave == 0 && present) atomicAdd(&cc[n], part);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  shift_copies();
+  __syncthreads();
+
+  uint32_t sumLH, Cv;
+  const int s = wave;
+  const int xn = xa + 64 * gx + 4 * n + s;
+  {
+    const int tly = tly0 + 8 * h;
+    int lo = max(tly - S, 0), hi = min(tly + S, H - 8);
+    if (h >= nbr) { lo = 1; hi = 0; }
+    sumLH = (uint32_t)(lo + hi);
+    Cv = 0x80000000u - (uint32_t)(hi - lo) - 1u;
+  }
+  const int u = xn - X0, sig = u & 3, ccol = u - sig;
+  v4i initv;
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const int tlx = tlx0 + 8 * r;
+    const int dx = xn - tlx;
+    const bool ok = r < nbc && dx >= max(-S, -tlx) && dx <= min(S, W - 8 - tlx);
+    const int c = cc[4 * h + r];
+    initv[r] = ok ? (c >> 1) : (c >> 1) + (1 << 22);
+  }
+  const uint32_t lbase = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) uint8_t*)smem);
+  const uint32_t lds_lane = lbase + (uint32_t)(sig * COPY + 2 * h * WP + ccol);
+  const uint32_t s2t_lane = (uint32_t)(uintptr_t)(
+      (__attribute__((address_space(3))) uint8_t*)s2t) + (uint32_t)(4 * n + s) * 4u;
+  typedef __attribute__((address_space(3))) const int lds_i32;
+
+  for (int ch = 0; ch < nch; ch++) {
+    const int y0 = ya + ch * L;
+    if (ch > 0) {
+      __syncthreads();
+      stage(y0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      shift_copies();
+      __syncthreads();
+    }
+    uint32_t best[4] = {~0u, ~0u, ~0u, ~0u};
+    uint32_t lp = lds_lane, sp = s2t_lane;
+    // F(row): window rows row + 2h, row + 2h + 1 (row & 3 static at every call)
+    auto load_row = [&](v4i& dst, auto ROW) {
+      constexpr int row = decltype(ROW)::value;
+      if constexpr ((row & 3) == 0 && row > 0) {
+        lp += 4 * WP;
+        asm volatile("" : "+v"(lp));
+      }
+      lds_u32* w0 = reinterpret_cast<lds_u32*>((uintptr_t)lp + (row & 3) * WP);
+      lds_u32* w1 = reinterpret_cast<lds_u32*>((uintptr_t)lp + ((row & 3) + 1) * WP);
+      dst[0] = (int)w0[0]; dst[1] = (int)w0[1]; dst[2] = (int)w1[0]; dst[3] = (int)w1[1];
+    };
+    auto epi = [&](int yrel, const v4i& av, int s2v) {
+      const uint32_t P = lshl6_add((uint32_t)s2v, (uint32_t)(64 + yrel));
+      const uint32_t Wd = sad_u32((uint32_t)(2 * (y0 + yrel)), sumLH, Cv);
+      const uint32_t Pf = (Wd & 0x80000000u) | P;
+      best[0] = min(best[0], ((uint32_t)av[0] << 7) + Pf);
+      best[1] = min(best[1], ((uint32_t)av[1] << 7) + Pf);
+      best[2] = min(best[2], ((uint32_t)av[2] << 7) + Pf);
+      best[3] = min(best[3], ((uint32_t)av[3] << 7) + Pf);
+    };
+    v4i fr[2];
+    int sv[2];
+    load_row(fr[0], std::integral_constant<int, 0>{});
+    sv[0] = *reinterpret_cast<lds_i32*>((uintptr_t)sp);
+    for (int k = 0; k < KM8; k++) {
+      sfor<0, 16>([&](auto II) {
+        constexpr int i = decltype(II)::value;
+        const int yrel = 16 * k + i;
+        load_row(fr[(i + 1) & 1], std::integral_constant<int, i + 1>{});
+        sv[(i + 1) & 1] = *reinterpret_cast<lds_i32*>((uintptr_t)(sp + (uint32_t)(i + 1) * RB));
+        const v4i acc = MFMA16(a, fr[i & 1], initv, 0, 0, 0);
+        epi(yrel, acc, sv[i & 1]);
+      });
+      sp += 16 * RB;
+      asm volatile("" : "+v"(sp));
+    }
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const uint32_t b = best[r];
+      if (b < (1u << 29)) {
+        const int m = 4 * h + r;
+        const uint32_t cost = (b >> 6) - 1u + (uint32_t)(cc[m] & 1);
+        const int dy = y0 + (int)(b & 63u) - (tly0 + 8 * h);
+        const int dx = xn - (tlx0 + 8 * r);
+        const unsigned long long key = ((unsigned long long)cost << 32) |
+                                       ((uint32_t)(dy + 32768) << 16) | (uint32_t)(dx + 32768);
+        atomicMin(&keys[m], key);
+      }
+    }
+  }
+  __syncthreads();
+  const int br = tid >> 2, bc = tid & 3;
+  const bool outb = tid < 16 && br < nbr && bc < nbc;
+  unsigned long long* gk = g.mkeys + 16 * (size_t)tile + tid;
+  bool last = ngx == 1;
+  if (!last) {
+    int* flag = reinterpret_cast<int*>(keys + 16);
+    if (outb) {
+      const unsigned long long old = __hip_atomic_fetch_min(gk, keys[tid], __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" : : "v"((uint32_t)old) : "memory");
+    }
+    __syncthreads();
+    if (tid == 0) {
+      const unsigned arrived = __hip_atomic_fetch_add(g.mcnt + tile, 1u, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT);
+      flag[0] = arrived == (unsigned)ngx - 1u;
+    }
+    __syncthreads();
+    last = flag[0] != 0;
+  }
+  if (last && outb) {
+    const unsigned long long kk =
+        ngx == 1 ? keys[tid]
+                 : __hip_atomic_exchange(gk, ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int out = (br0 + br - p.block_row_begin) * p.nbx + bc0 + bc;
+    p.mv[2 * out] = (int16_t)((int)(kk & 0xFFFF) - 32768);
+    p.mv[2 * out + 1] = (int16_t)((int)((kk >> 16) & 0xFFFF) - 32768);
+    if (p.cost) p.cost[out] = (uint32_t)(kk >> 32);
+  }
+  if (last && ngx > 1 && tid == 0)
+    __hip_atomic_store(g.mcnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 }  // namespace
 
 // Process-wide path switch (me_set_kernel_path): A/B tests and diagnostics.
@@ -650,8 +891,8 @@ bool mfma_disabled() {
 
 // Tiles of a B = 16 search over block rows [begin, end) (the merge buffers' size).
 size_t mfma_merge_tiles(const SearchArgs& p) {
-  if (p.blk != 16 || p.width < 16) return 0;
-  const size_t tx = (size_t)((p.width / 16 + 3) / 4);
+  if ((p.blk != 16 && p.blk != 8) || p.width < p.blk) return 0;
+  const size_t tx = (size_t)((p.width / p.blk + 3) / 4);
   const size_t ty = (size_t)((p.block_row_end - p.block_row_begin + 3) / 4);
   return tx * ty;
 }
@@ -664,8 +905,12 @@ size_t mfma_ssd_scratch(const SearchArgs& p) {
 
 // Full-height block rows [row0, row0 + nrows) and full-width columns of a B = 16
 // SSD search; the caller routes partial rows / columns to the VALU kernels.
+static bool plan_mfma_ssd8(const SearchArgs& p, MfmaGeom* g);
+
 bool plan_mfma_ssd(const SearchArgs& p, MfmaGeom* g) {
-  if (p.cost_kind != COST_SSD || p.blk != 16) return false;
+  if (p.cost_kind != COST_SSD) return false;
+  if (p.blk == 8) return plan_mfma_ssd8(p, g);
+  if (p.blk != 16) return false;
   if (mfma_disabled()) return false;
   const int S = p.range, W = p.width, H = p.height;
   if (S < 1 || W < 16 || H < 16) return false;
@@ -744,13 +989,74 @@ bool plan_mfma_ssd(const SearchArgs& p, MfmaGeom* g) {
   return true;
 }
 
+// 8x8 blocks: full-height block rows only (a partial bottom row goes to the
+// VALU kernels), one 64-column group per workgroup, chunks of 64 rows.
+static bool plan_mfma_ssd8(const SearchArgs& p, MfmaGeom* g) {
+  if (mfma_disabled()) return false;
+  const int S = p.range, W = p.width, H = p.height;
+  if (S < 1 || W < 8 || H < 8) return false;
+  if (p.stride % 4 || (uintptr_t)p.cur % 4 || (uintptr_t)p.ref % 4) return false;
+  const int nby = (H + 7) / 8;
+  const int r0 = p.block_row_begin;
+  int r1 = p.block_row_end;
+  if (r1 == nby && H % 8) r1--;
+  g->row0 = r0;
+  g->nrows = r1 - r0;
+  if (g->nrows <= 0) return false;
+  g->hb = 8;
+  g->hb_row = -1;
+  g->nbx = W / 8;
+  g->tiles_x = (g->nbx + 3) / 4;
+  g->tiles_y = (g->nrows + 3) / 4;
+  const int nxmax = min(24 + 2 * S + 1, W - 7);
+  g->ngx = (nxmax + 63) / 64;
+  g->ngxw = 1;
+  if (g->ngx > 1 && (!p.mkeys || !p.mcnt || p.merge_tiles < mfma_merge_tiles(p))) return false;
+  g->km = 4;  // L = 64
+  const int L = 16 * g->km;
+  g->lds = 4 * (L + 8) * 96 + 16 * 8 + 16 * 4 + (L + 1) * 256;
+  g->ya0 = max(r0 * 8 - S, 0);
+  const int ya1 = min(r1 * 8 + S, H);
+  g->rp_rows = ya1 - g->ya0;
+  g->pitch = (W + 15) & ~15;
+  g->rows_alloc = g->rp_rows + 80;
+  g->s2h_row0 = 0;
+  const size_t plane = (size_t)g->rows_alloc * g->pitch;
+  const size_t rp_alloc = (plane + 255) & ~(size_t)255;
+  const size_t s2_plane = plane * 4;
+  if (rp_alloc + s2_plane >= (1ull << 31)) return false;
+  g->rp_bytes = (uint32_t)plane;
+  g->s2_bytes = (uint32_t)s2_plane;
+  g->s2h_off = 0;
+  g->scratch_bytes = rp_alloc + s2_plane;
+  g->rp = reinterpret_cast<int8_t*>(p.scratch);
+  g->s2 = p.scratch ? reinterpret_cast<int*>(p.scratch + rp_alloc) : nullptr;
+  g->s2h = nullptr;
+  g->mkeys = p.mkeys;
+  g->mcnt = p.mcnt;
+  return true;
+}
+
 hipError_t launch_mfma_ssd(const SearchArgs& p, const MfmaGeom& g, hipStream_t stream) {
   const int nmain = (g.rows_alloc + 63) / 64;
-  const int nh = g.hb < 16 ? (g.rows_alloc - g.s2h_row0 + 63) / 64 : 0;
+  const int nh = g.hb_row >= 0 ? (g.rows_alloc - g.s2h_row0 + 63) / 64 : 0;
   dim3 pgrid((unsigned)((g.pitch + 63) / 64), (unsigned)(nmain + nh));
-  hipLaunchKernelGGL(me_ssd_prep_kernel, pgrid, dim3(256), 0, stream, p, g);
+  if (p.blk == 8)
+    hipLaunchKernelGGL(me_ssd_prep_kernel<8>, pgrid, dim3(256), 0, stream, p, g);
+  else
+    hipLaunchKernelGGL(me_ssd_prep_kernel<16>, pgrid, dim3(256), 0, stream, p, g);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
+  if (p.blk == 8) {
+    const dim3 grid8((unsigned)(g.tiles_x * g.tiles_y * g.ngx));
+    if (g.lds > 64 * 1024) {
+      e = hipFuncSetAttribute((const void*)me_mfma_ssd8_kernel<4>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, g.lds);
+      if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(me_mfma_ssd8_kernel<4>, grid8, dim3(256), g.lds, stream, p, g);
+    return hipGetLastError();
+  }
   const int wpt = (g.ngx + g.ngxw - 1) / g.ngxw;
   const dim3 grid((unsigned)(g.tiles_x * g.tiles_y * wpt));
 #define ME_MFMA_CASE(NG, KK)                                                              \

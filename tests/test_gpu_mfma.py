@@ -120,3 +120,56 @@ def test_mfma_stripes_halo_only(engine):
         sl = slice(r0 * nbx, r1 * nbx)
         np.testing.assert_array_equal(mvt.cpu().numpy(), omv[sl], err_msg=f"rows {r0}-{r1}")
         np.testing.assert_array_equal(cot.cpu().numpy().view(np.uint32), ocost[sl])
+
+
+# ------------------------------------------------------------------ 8x8 blocks
+def _check8(engine, ref, cur, span, tag):
+    mv, cost = engine.full_search(ref, cur, 8, span, "ssd")
+    omv, ocost, _ = O.full_search(ref, cur, 8, span, "ssd", threads=NT)
+    np.testing.assert_array_equal(mv, omv, err_msg=tag)
+    np.testing.assert_array_equal(cost, ocost, err_msg=tag)
+
+
+@pytest.mark.parametrize("span", [1, 2, 5, 8, 13, 20, 32, 33, 40, 64, 100, 128])
+def test_mfma8_ssd_spans(engine, span):
+    """8x8 blocks (one MFMA per output tile): tiles of 4x4 blocks, one to five
+    64-column groups per tile (merged across workgroups), partial bottom rows
+    and right columns beside the MFMA tiles."""
+    rng = np.random.default_rng(2000 + span)
+    for (h, w) in [(72, 96), (150, 200), (64, 352), (53, 101)]:
+        ref, cur = _pair(rng, h, w, dx=(span % 5) - 2, dy=2 - (span % 3))
+        _check8(engine, ref, cur, span, f"B8 {h}x{w} S{span}")
+
+
+def test_mfma8_vs_valu_and_extremes(engine):
+    rng = np.random.default_rng(9)
+    try:
+        for (h, w, span) in [(288, 352, 16), (200, 320, 48), (160, 240, 128)]:
+            ref, cur = _pair(rng, h, w, dx=-3, dy=2)
+            me.set_kernel_path("auto")
+            a = engine.full_search(ref, cur, 8, span, "ssd")
+            me.set_kernel_path("valu")
+            b = engine.full_search(ref, cur, 8, span, "ssd")
+            np.testing.assert_array_equal(a[0], b[0], err_msg=f"{h}x{w} S{span}")
+            np.testing.assert_array_equal(a[1], b[1])
+    finally:
+        me.set_kernel_path("auto")
+    h, w = 64, 104
+    zeros, full = np.zeros((h, w), np.uint8), np.full((h, w), 255, np.uint8)
+    noise = rng.integers(0, 256, (h, w), dtype=np.uint8)
+    for tag, ref, cur in [("flat", full, full), ("max", zeros, full), ("max2", full, zeros),
+                          ("noise/0", noise, zeros), ("noise", noise, noise)]:
+        _check8(engine, ref, cur, 20, f"B8 {tag}")
+
+
+def test_mfma8_8k_s128_sampled(engine):
+    """BASELINE configs[4] shape with the reference's cost: 7680x4320, 8x8,
+    +-128 SSD on the matrix cores, oracle on sampled block rows."""
+    ref, cur = synth.named_pair("8k")
+    mv, cost = engine.full_search(ref, cur, 8, 128, "ssd")
+    nbx = 960
+    for row in (0, 301, 539):
+        b0, b1 = row * nbx + 400, row * nbx + 448
+        omv, ocost, _ = O.full_search(ref, cur, 8, 128, "ssd", threads=NT, begin=b0, end=b1)
+        np.testing.assert_array_equal(mv[b0:b1], omv, err_msg=f"row {row}")
+        np.testing.assert_array_equal(cost[b0:b1], ocost)
