@@ -696,6 +696,9 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd8_kernel(SearchArgs p, M
       return (uint32_t)(base + rho * g.pitch + k);
     });
     const int sbase = ((y0 - g.ya0) * g.pitch + xa + 64 * gx) * 4;
+#if ME_MFMA_ABLATE & 1  // diagnostic: no S2 table staging
+    if (opaque(0))
+#endif
     dma16(rs2, s2t, L * RB, [&](int d) {
       const int rho = d / RB, k = d - rho * RB;
       return (uint32_t)(sbase + rho * g.pitch * 4 + k);
@@ -782,7 +785,11 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd8_kernel(SearchArgs p, M
 
   for (int ch = 0; ch < nch; ch++) {
     const int y0 = ya + ch * L;
+#if ME_MFMA_ABLATE & 4  // diagnostic: only the first chunk staged
+    if (opaque(0)) {
+#else
     if (ch > 0) {
+#endif
       __syncthreads();
       stage(y0);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -792,42 +799,72 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd8_kernel(SearchArgs p, M
     }
     uint32_t best[4] = {~0u, ~0u, ~0u, ~0u};
     uint32_t lp = lds_lane, sp = s2t_lane;
-    // F(row): window rows row + 2h, row + 2h + 1 (row & 3 static at every call)
-    auto load_row = [&](v4i& dst, auto ROW) {
+    // One window row (8 bytes at x_n) of lane group h: window row row + 2h.  Step
+    // t's fragment is rows t + 2h, t + 2h + 1, so consecutive steps share a row:
+    // one new row per step (row & 3 static at every call; lp moves every 4 rows).
+    typedef int v2i __attribute__((ext_vector_type(2)));
+    auto load_row = [&](v2i& dst, auto ROW) {
       constexpr int row = decltype(ROW)::value;
       if constexpr ((row & 3) == 0 && row > 0) {
         lp += 4 * WP;
         asm volatile("" : "+v"(lp));
       }
       lds_u32* w0 = reinterpret_cast<lds_u32*>((uintptr_t)lp + (row & 3) * WP);
-      lds_u32* w1 = reinterpret_cast<lds_u32*>((uintptr_t)lp + ((row & 3) + 1) * WP);
-      dst[0] = (int)w0[0]; dst[1] = (int)w0[1]; dst[2] = (int)w1[0]; dst[3] = (int)w1[1];
+      dst[0] = (int)w0[0]; dst[1] = (int)w0[1];
     };
-    auto epi = [&](int yrel, const v4i& av, int s2v) {
-      const uint32_t P = lshl6_add((uint32_t)s2v, (uint32_t)(64 + yrel));
-      const uint32_t Wd = sad_u32((uint32_t)(2 * (y0 + yrel)), sumLH, Cv);
-      const uint32_t Pf = (Wd & 0x80000000u) | P;
-      best[0] = min(best[0], ((uint32_t)av[0] << 7) + Pf);
-      best[1] = min(best[1], ((uint32_t)av[1] << 7) + Pf);
-      best[2] = min(best[2], ((uint32_t)av[2] << 7) + Pf);
-      best[3] = min(best[3], ((uint32_t)av[3] << 7) + Pf);
+    // Keys of one step; steps pair up into one v_min3 per block.  MASKED = false
+    // on chunks where every lane group's block row is valid for every row
+    // (the middle of a tile's range): no y test at all.
+    auto keys_of = [&](int yrel, const v4i& av, int s2v, uint32_t (&k)[4], auto MASKED) {
+      uint32_t Pf = lshl6_add((uint32_t)s2v, (uint32_t)(64 + yrel));
+      if constexpr (decltype(MASKED)::value) {
+        const uint32_t Wd = sad_u32((uint32_t)(2 * (y0 + yrel)), sumLH, Cv);
+        Pf = (Wd & 0x80000000u) | Pf;
+      }
+#if ME_MFMA_ABLATE & 2  // diagnostic: epilogue cut to the accumulator
+      for (int r = 0; r < 4; r++) k[r] = (uint32_t)av[r];
+      (void)Pf;
+#else
+#pragma unroll
+      for (int r = 0; r < 4; r++) k[r] = ((uint32_t)av[r] << 7) + Pf;
+#endif
     };
-    v4i fr[2];
-    int sv[2];
-    load_row(fr[0], std::integral_constant<int, 0>{});
-    sv[0] = *reinterpret_cast<lds_i32*>((uintptr_t)sp);
-    for (int k = 0; k < KM8; k++) {
-      sfor<0, 16>([&](auto II) {
-        constexpr int i = decltype(II)::value;
-        const int yrel = 16 * k + i;
-        load_row(fr[(i + 1) & 1], std::integral_constant<int, i + 1>{});
-        sv[(i + 1) & 1] = *reinterpret_cast<lds_i32*>((uintptr_t)(sp + (uint32_t)(i + 1) * RB));
-        const v4i acc = MFMA16(a, fr[i & 1], initv, 0, 0, 0);
-        epi(yrel, acc, sv[i & 1]);
+    auto body = [&](auto MASKED) {
+      v2i rw[3];  // window rows t+2h (older), t+2h+1, and the prefetched t+2h+2
+      int sv[2];
+      uint32_t kp[4];
+      load_row(rw[0], std::integral_constant<int, 0>{});
+      load_row(rw[1], std::integral_constant<int, 1>{});
+      sv[0] = *reinterpret_cast<lds_i32*>((uintptr_t)sp);
+      // fully unrolled: the 3-row ring index t % 3 must be static
+      sfor<0, L>([&](auto TT) {
+        constexpr int t = decltype(TT)::value;
+        // rows t+2h in rw[t % 3], t+2h+1 in rw[(t+1) % 3]; prefetch t+2h+2
+        load_row(rw[(t + 2) % 3], std::integral_constant<int, t + 2>{});
+        if constexpr (t + 1 < L)
+          sv[(t + 1) & 1] = *reinterpret_cast<lds_i32*>((uintptr_t)(sp + (uint32_t)(t + 1) * RB));
+        const v2i r0 = rw[t % 3], r1 = rw[(t + 1) % 3];
+        const v4i f = {r0[0], r0[1], r1[0], r1[1]};
+        const v4i acc = MFMA16(a, f, initv, 0, 0, 0);
+        if constexpr ((t & 1) == 0) {
+          keys_of(t, acc, sv[t & 1], kp, MASKED);
+        } else {
+          uint32_t kc[4];
+          keys_of(t, acc, sv[t & 1], kc, MASKED);
+#pragma unroll
+          for (int r = 0; r < 4; r++) best[r] = min(best[r], min(kp[r], kc[r]));
+        }
       });
-      sp += 16 * RB;
-      asm volatile("" : "+v"(sp));
+    };
+    // every block row present and valid on all L rows of this chunk?
+    bool full = nbr == 4;
+#pragma unroll
+    for (int hh = 0; hh < 4; hh++) {
+      const int tly = tly0 + 8 * hh;
+      full = full && max(tly - S, 0) <= y0 && min(tly + S, H - 8) >= y0 + L - 1;
     }
+    if (full) body(std::false_type{});
+    else body(std::true_type{});
 #pragma unroll
     for (int r = 0; r < 4; r++) {
       const uint32_t b = best[r];

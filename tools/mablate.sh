@@ -13,7 +13,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 for lib in libme_hip.so $(cd motionestimation_amd/lib && ls libme_hip_mabl*.so libme_hip_mdly*.so); do
   d=$R/gpurun_out/mabl_$lib
-  (cd /tmp && ME_HIP_LIB=$lib timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $d -o run --output-format csv -- python3 $R/tools/size_sweep.py --cost ssd --heights 1080 --iters 50 > $d.log 2>&1)
+  (cd /tmp && ME_HIP_LIB=$lib timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $d -o run --output-format csv -- python3 $R/tools/size_sweep.py ${SWEEP_ARGS:---cost ssd --heights 1080 --iters 50} > $d.log 2>&1)
   echo "== $lib" >> $out
   find $d -name "*kernel_stats.csv" | xargs cat | awk -F'","' 'NR>1{printf "%-40s %s\n", substr($1,1,40), $4}' >> $out
 done
