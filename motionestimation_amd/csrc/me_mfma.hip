@@ -913,6 +913,345 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd8_kernel(SearchArgs p, M
     __hip_atomic_store(g.mcnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// ------------------------------------------------- 16x16, block-major tiles
+// One block per GEMM instead of 16: the output tile is 16 x positions (M,
+// x = 16 i + m) by 16 y positions (N, y = Ys + n) of ONE block, so every output
+// is a candidate of that block (the 4x4-block tiles above compute 27 % useful
+// outputs at S = 32; here the waste is only the range's 16-alignment).  K = 64
+// = 2 block rows x a 32-byte window span: lane (m, h) of A holds block row
+// 2q + (h >> 1) shifted right by m bytes inside the span (bytes 16 (h & 1) ..
+// +15 of [0^m, c''_row, 0...]), so half of K is zero -- 8 MFMAs per output
+// tile.  B is 16 window bytes at row Ys + n + 2q + (h >> 1), column 16 i +
+// 16 (h & 1): one aligned ds_read_b128, no shifted copies.  A wave holds two
+// horizontally adjacent blocks (A in 64 VGPRs) that share each B fragment and
+// each S2 load; a workgroup = 4 waves = 8 blocks of one block row, whose
+// window (rows [ylo, ylo + 16 Ty + 15), 16-aligned columns) is DMA'd once:
+// no chunks, no cross-workgroup merge.
+//   lane (n, h), result r: position x = 16 i + 4 h + r, y = Ys + n
+//   key = ((2 X + S2 + 1 + 2^23) << 6) + 4 (i - iu0) + r
+//       = (X << 7) + ((S2 << 6) + 2^29 + 64 + 4 (i - iu0) + r)
+// 2 X + S2 = SSD - Cc with Cc <= 2^22, so valid keys lie in (0, 2^31), and any
+// window content keeps 2 X + S2 + 1 + 2^23 in (0, 2^25): positions outside
+// the block's x range get 2^24 added to the accumulator (key + 2^31, first and
+// last tile only) and can never win.  y bands of 16 rows; the last band ends at
+// the range's last row (overlapping its predecessor), so no y mask.  Per band
+// the lane's best is widened to (key >> 6, s << 6 | idx), which orders by SSD,
+// then dy, then dx (the raster-first rule); the lanes meet in a 64-bit LDS min.
+constexpr int BM_LP = 288;    // window row pitch (16-byte slots 2n + (h & 1) mod 16: conflict-free b128)
+constexpr int BM_CREC = 48;   // cur row record: 16 zero bytes, the row (c ^ 0x7F), 16 zero bytes
+constexpr int BM_HDR = 8 * 16 * BM_CREC + 8 * 8 + 8 * 4;  // records, keys, cc
+constexpr int BM_WINB = 31 * BM_LP;  // one band's window rows
+
+__global__ __launch_bounds__(256)
+__attribute__((amdgpu_waves_per_eu(4))) void me_mfma_bm16_kernel(SearchArgs p, MfmaGeom g) {
+  extern __shared__ __align__(16) uint8_t smem[];
+  uint8_t* crec = smem;
+  unsigned long long* keys = reinterpret_cast<unsigned long long*>(smem + 8 * 16 * BM_CREC);
+  int* cc = reinterpret_cast<int*>(smem + 8 * 16 * BM_CREC + 64);
+  uint8_t* win = smem + BM_HDR;
+
+  const int tid = (int)threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int n = lane & 15, h = lane >> 4;
+  const int S = p.range, W = p.width, H = p.height;
+  int lin;
+  {  // XCD-banded: XCD x walks one contiguous run of strips
+    const int nwg = (int)gridDim.x, bid = (int)blockIdx.x;
+    const int x = bid & 7, m = bid >> 3, q = nwg >> 3, rem = nwg & 7;
+    lin = x * q + min(x, rem) + m;
+  }
+  const int brl = lin / g.bm_wpr, sx = lin - brl * g.bm_wpr;
+  const int br = g.row0 + brl;
+  const int bc0 = 8 * sx, nb = min(8, g.nbx - bc0);
+  const int by = 16 * br, bh = br == g.hb_row ? g.hb : 16;
+  const int ylo = max(by - S, 0), yhi = min(by + S, H - bh);
+  const int Ty = (yhi - ylo + 16) >> 4;
+  const int tc0 = max(16 * bc0 - S, 0) >> 4;
+  // y bands of 16 rows; when the range has >= 16 rows the last band ends at yhi
+  // (it overlaps the one before: no row past yhi is ever computed)
+  const bool yover = yhi - ylo >= 15;
+  auto band_y = [&](int s) { return yover ? min(ylo + 16 * s, yhi - 15) : ylo + 16 * s; };
+  // band window: frame rows [Ys, Ys + 31) x columns [16 tc0, 16 tc0 + BM_LP),
+  // double-buffered (band s + 1 arrives by LDS DMA while band s computes)
+  const __amdgpu_buffer_rsrc_t rrp =
+      __builtin_amdgcn_make_buffer_rsrc((void*)g.rp, (short)0, g.rp_bytes, 0x00020000);
+  auto stage_band = [&](int s) {
+    const int gbase = (band_y(s) - g.ya0) * g.pitch + 16 * tc0;
+    dma16(rrp, win + (s & 1) * BM_WINB, BM_WINB, [&](int d) {
+      const int rho = d / BM_LP, k = d - rho * BM_LP;
+      return (uint32_t)(gbase + rho * g.pitch + k);
+    });
+  };
+
+  MS_STAMP(0, __builtin_amdgcn_s_memtime());
+  MS_STAMP(6, __builtin_amdgcn_s_memrealtime());
+  if (tid < 8) {
+    keys[tid] = ~0ull;
+    cc[tid] = 0;
+  }
+  stage_band(0);
+  __syncthreads();  // keys / cc initialised
+  if (tid < 128) {  // cur row records and Cc = sum(c''^2 + 2 c'')
+    const int j = tid >> 4, rho = tid & 15;
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if (j < nb && rho < bh) {
+      const u32x4* src = reinterpret_cast<const u32x4*>(
+          p.cur + (ptrdiff_t)(by + rho - p.cur_row0) * p.stride + 16 * (bc0 + j));
+      v = *src ^ 0x7F7F7F7Fu;
+    }
+    const u32x4 z = {0u, 0u, 0u, 0u};
+    u32x4* rec = reinterpret_cast<u32x4*>(crec + (16 * j + rho) * BM_CREC);
+    rec[0] = z;
+    rec[1] = v;
+    rec[2] = z;
+    int part = 0;
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+      part = __builtin_amdgcn_sdot4((int)v[e], (int)v[e], part, false);
+      part = __builtin_amdgcn_sdot4((int)v[e], 0x02020202, part, false);
+    }
+    if (j < nb) atomicAdd(&cc[j], part);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  const int j0 = 2 * wave, j1 = j0 + 1;
+  const bool hasA = j0 < nb, hasB = j1 < nb;
+  // per block: tile range [i0, i1] (16-aligned positions) and x range [xlo, xhi]
+  const int bxA = 16 * (bc0 + j0), bxB = bxA + 16;
+  const int xloA = max(bxA - S, 0), xhiA = min(bxA + S, W - 16);
+  const int xloB = max(bxB - S, 0), xhiB = min(bxB + S, W - 16);
+  const int i0A = xloA >> 4, i1A = xhiA >> 4, i0B = xloB >> 4, i1B = xhiB >> 4;
+  const int iu0 = i0A, iu1 = hasB ? i1B : i1A;
+
+  // A fragments: bytes o .. o + 15 of record row 2q + (h >> 1), o = 16 + 16 (h & 1) - m
+  v4i aA[8], aB[8];
+  {
+    const int o = 16 + 16 * (h & 1) - n, sh = o & 3;
+    typedef __attribute__((address_space(3))) const uint32_t lds_c32;
+    const uint32_t lb = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) uint8_t*)crec) +
+                        (uint32_t)((h >> 1) * BM_CREC + (o & ~3));
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+#pragma unroll
+      for (int bsel = 0; bsel < 2; bsel++) {
+        const uint32_t a0 = lb + (uint32_t)(((2 * wave + bsel) * 16 + 2 * q) * BM_CREC);
+        uint32_t d[5];
+#pragma unroll
+        for (int e = 0; e < 5; e++) d[e] = *reinterpret_cast<lds_c32*>((uintptr_t)(a0 + 4 * e));
+        v4i f;
+#pragma unroll
+        for (int e = 0; e < 4; e++) f[e] = (int)__builtin_amdgcn_alignbyte(d[e + 1], d[e], sh);
+        if (bsel == 0) aA[q] = f; else aB[q] = f;
+      }
+    }
+  }
+  MS_STAMP(1, __builtin_amdgcn_s_memtime());
+  const int ccA = hasA ? cc[j0] : 0, ccB = hasB ? cc[j1] : 0;
+  // Masks of a block's first / last tile: 2^24 on the accumulator of positions
+  // outside [xlo, xhi] (bit 31 of the key).
+  // Bit 4 e + r of mbits: result r of edge e (A first, A last, B first, B last).
+  uint32_t mbits = 0;
+  {
+    auto xmask = [&](int e, int i, int xlo, int xhi) {
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int x = 16 * i + 4 * h + r;
+        if (x < xlo || x > xhi) mbits |= 1u << (4 * e + r);
+      }
+    };
+    xmask(0, i0A, xloA, xhiA);
+    xmask(1, i1A, xloA, xhiA);
+    xmask(2, i0B, xloB, xhiB);
+    xmask(3, i1B, xloB, xhiB);
+  }
+  const uint32_t ym = (!yover && n > yhi - ylo) ? 0x80000000u : 0u;  // OR-ed into the key
+  // Interior pairs (both blocks' x ranges inside the frame, >= 3 tiles each,
+  // full 16-row bands) take the mask-free fast path; their only invalid
+  // positions are the range ends inside the first and the last tile, the
+  // same lanes for every such block: m < (bx - S) & 15, m > (bx + S) & 15.
+  const bool fast = hasB && yover && bxA - S >= 0 && bxB + S <= W - 16 && i1A - i0A >= 2;
+  const int mfa = (bxA - S) & 15, mlb = (bxA + S) & 15;
+  // built in the edge tiles (a few VALU there) rather than held in 8 VGPRs
+  auto edge_mask = [&](auto LAST) {
+    v4i mk;
+    const int m4 = opaque(4 * h);  // recomputed per use, not hoisted and spilled
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const int m = m4 + r;
+      mk[r] = (decltype(LAST)::value ? m > mlb : m < mfa) ? (1 << 24) : 0;
+    }
+    return mk;
+  };
+
+  const __amdgpu_buffer_rsrc_t rs2 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)g.s2, (short)0, g.s2_bytes, 0x00020000);
+  const int s2v = (n * g.pitch + 4 * h) * 4 + (br == g.hb_row ? (int)g.s2h_off : 0);
+  const uint32_t lbase = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) uint8_t*)win) +
+                         (uint32_t)((n + (h >> 1)) * BM_LP + 16 * (h & 1) - 16 * tc0);
+  typedef __attribute__((address_space(3))) const v4i lds_v4i;
+  const v4i zero4 = {0, 0, 0, 0};
+
+  unsigned long long bestA = ~0ull, bestB = ~0ull;  // (key >> 6) << 32 | s << 6 | idx
+  for (int s = 0; s < Ty; s++) {
+    if (s + 1 < Ty) stage_band(s + 1);
+    if (hasA) {
+      const int Ys = band_y(s);
+      const uint32_t lrow0 = lbase + (uint32_t)((s & 1) * BM_WINB);
+      const int srow = (Ys - g.ya0) * g.pitch * 4;
+      uint32_t bA = ~0u, bB = ~0u;
+      // One 16 x 16 output tile per block at window column 16 i.  MA / MB: the
+      // mask of block A / B on this tile -- 0 none, 1 the first-tile mask mF, 2
+      // the last-tile mask mL (both as the first MFMA's accumulator input, no
+      // VALU), 3 the generic path (mbits, ym: frame-clipped pairs, tiny ranges).
+      auto tile = [&](int i, auto DA, auto DB, auto MA, auto MB) {
+        constexpr bool da = decltype(DA)::value, db = decltype(DB)::value;
+        constexpr int ma = decltype(MA)::value, mb = decltype(MB)::value;
+#if ME_MFMA_ABLATE & 256  // diagnostic: no S2 loads
+        const v4i s2c = {n, h, s, i};
+#else
+        const v4i s2c = __builtin_bit_cast(
+            v4i, __builtin_amdgcn_raw_buffer_load_b128(rs2, s2v, srow + 64 * i, 0));
+#endif
+        const uint32_t lrow = lrow0 + (uint32_t)(16 * i);
+        v4i accA = zero4, accB = zero4;
+        if constexpr (ma == 1 || ma == 2) accA = edge_mask(std::integral_constant<bool, ma == 2>{});
+        if constexpr (mb == 1 || mb == 2) accB = edge_mask(std::integral_constant<bool, mb == 2>{});
+        // Fragments in pairs, the next pair in flight during this pair's MFMAs
+        // (four fragments live: the A fragments hold 64 VGPRs).
+        auto ld = [&](int q) {
+#if ME_MFMA_ABLATE & 2048  // diagnostic: no fragment loads
+          const v4i t = {(int)lrow, q, 0, 0};
+          return t;
+#else
+          return *reinterpret_cast<lds_v4i*>((uintptr_t)(lrow + (uint32_t)(2 * q * BM_LP)));
+#endif
+        };
+        v4i f0 = ld(0), f1 = ld(1);
+#pragma unroll
+        for (int qp = 0; qp < 4; qp++) {
+          v4i n0 = f0, n1 = f1;
+          if (qp < 3) {
+            n0 = ld(2 * qp + 2);
+            n1 = ld(2 * qp + 3);
+          }
+          if constexpr (da) accA = MFMA16(aA[2 * qp], f0, accA, 0, 0, 0);
+          if constexpr (db) accB = MFMA16(aB[2 * qp], f0, accB, 0, 0, 0);
+          if constexpr (da) accA = MFMA16(aA[2 * qp + 1], f1, accA, 0, 0, 0);
+          if constexpr (db) accB = MFMA16(aB[2 * qp + 1], f1, accB, 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
+          f0 = n0;
+          f1 = n1;
+        }
+        // key = ((2 acc + S2 + 1 + 2^23) << 6) + 4 (i - iu0) + r, acc = X (+ masks):
+        // one v_lshl_add for the shared position term, one per key
+        const uint32_t kb = (1u << 29) + 64u + 4u * (uint32_t)(i - iu0);
+        uint32_t P[4];
+#pragma unroll
+        for (int r = 0; r < 4; r++) P[r] = lshl6_add((uint32_t)s2c[r], kb + (uint32_t)r);
+        auto keys_of = [&](v4i acc, uint32_t& best, int i0, int i1, int e0, auto GEN) {
+          if constexpr (decltype(GEN)::value) {
+            if (i == i0 || i == i1) {
+              const int e = i == i0 ? e0 : e0 + 1;
+              const uint32_t mb4 = (uint32_t)opaque((int)mbits);  // not hoisted: no 16 VGPRs of masks
+#pragma unroll
+              for (int r = 0; r < 4; r++)
+                acc[r] += (int)(__builtin_amdgcn_ubfe(mb4, (uint32_t)(4 * e + r), 1u) << 24);
+            }
+          }
+#if ME_MFMA_ABLATE & 512  // diagnostic: epilogue cut to one min
+          best = min(best, (uint32_t)(acc[0] ^ acc[1] ^ acc[2] ^ acc[3]) ^ P[0]);
+          return;
+#endif
+          uint32_t k[4];
+#pragma unroll
+          for (int r = 0; r < 4; r++) k[r] = ((uint32_t)acc[r] << 7) + P[r];
+          if constexpr (decltype(GEN)::value) {
+#pragma unroll
+            for (int r = 0; r < 4; r++) k[r] |= ym;
+          }
+          best = min(best, min(k[0], k[1]));
+          best = min(best, min(k[2], k[3]));
+        };
+        if constexpr (da) keys_of(accA, bA, i0A, i1A, 0, std::integral_constant<bool, ma == 3>{});
+        if constexpr (db) keys_of(accB, bB, i0B, i1B, 2, std::integral_constant<bool, mb == 3>{});
+      };
+      using T_ = std::true_type;
+      using F_ = std::false_type;
+      using M0 = std::integral_constant<int, 0>;
+      using M1 = std::integral_constant<int, 1>;
+      using M2 = std::integral_constant<int, 2>;
+      using M3 = std::integral_constant<int, 3>;
+      if (fast) {
+        // interior pair: A's tiles i0A .. i1A, B's one to the right
+        tile(i0A, T_{}, F_{}, M1{}, M0{});
+        tile(i0A + 1, T_{}, T_{}, M0{}, M1{});
+        for (int i = i0A + 2; i < i1A; i++) tile(i, T_{}, T_{}, M0{}, M0{});
+        tile(i1A, T_{}, T_{}, M2{}, M0{});
+        tile(i1B, F_{}, T_{}, M0{}, M2{});
+      } else {
+        for (int i = iu0; i <= iu1; i++) {
+          const bool useA = i <= i1A, useB = hasB && i >= i0B;
+          if (useA && useB) tile(i, T_{}, T_{}, M3{}, M3{});
+          else if (useA) tile(i, T_{}, F_{}, M3{}, M3{});
+          else tile(i, F_{}, T_{}, M3{}, M3{});
+        }
+      }
+      // end of the band: widen; the strictly better key wins (an earlier band, a
+      // smaller dy, keeps ties)
+      const unsigned long long kA = ((unsigned long long)(bA >> 6) << 32) | ((uint32_t)s << 6) | (bA & 63u);
+      const unsigned long long kB = ((unsigned long long)(bB >> 6) << 32) | ((uint32_t)s << 6) | (bB & 63u);
+      bestA = (kA >> 32) < (bestA >> 32) ? kA : bestA;
+      bestB = (kB >> 32) < (bestB >> 32) ? kB : bestB;
+    }
+    if (s == 0) MS_STAMP(2, __builtin_amdgcn_s_memtime());
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // band s + 1 landed (this thread's pieces)
+    __syncthreads();                                   // ... and everyone's; band s free
+  }
+  if (hasA) {
+    auto emit = [&](unsigned long long b, int j, int ccj, int bx) {
+      const uint32_t hi = (uint32_t)(b >> 32);
+      if (hi < (1u << 25)) {
+        const uint32_t lo = (uint32_t)b;
+        const int sb = (int)(lo >> 6), idx = (int)(lo & 63u);
+        const uint32_t cost = hi - 1u - (1u << 23) + (uint32_t)ccj;
+        const int dx = 16 * (iu0 + (idx >> 2)) + 4 * h + (idx & 3) - bx;
+        const int dy = band_y(sb) + n - by;
+        const unsigned long long key = ((unsigned long long)cost << 32) |
+                                       ((uint32_t)(dy + 32768) << 16) | (uint32_t)(dx + 32768);
+        // per-lane LDS atomic (the compiler's wave-scan expansion of a
+        // uniform-address atomicMin is a 64-step readlane loop)
+        const uint32_t a = (uint32_t)(uintptr_t)(
+            (__attribute__((address_space(3))) unsigned long long*)(keys + j));
+        asm volatile("ds_min_u64 %0, %1" : : "v"(a), "v"(key) : "memory");
+      }
+    };
+    emit(bestA, j0, ccA, bxA);
+    if (hasB) emit(bestB, j1, ccB, bxB);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+#ifdef ME_STAMPS
+  if (tid == 0 && blockIdx.x < (1u << 14)) {
+    unsigned hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    g_mstamps[8 * blockIdx.x + 3] = __builtin_amdgcn_s_memtime();
+    g_mstamps[8 * blockIdx.x + 4] = hw;
+    g_mstamps[8 * blockIdx.x + 5] = xcc;
+    g_mstamps[8 * blockIdx.x + 7] = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
+  if (tid < nb) {
+    const unsigned long long kk = keys[tid];
+    const int out = (br - p.block_row_begin) * p.nbx + bc0 + tid;
+    p.mv[2 * out] = (int16_t)((int)(kk & 0xFFFF) - 32768);
+    p.mv[2 * out + 1] = (int16_t)((int)((kk >> 16) & 0xFFFF) - 32768);
+    if (p.cost) p.cost[out] = (uint32_t)(kk >> 32);
+  }
+}
+
 }  // namespace
 
 // Process-wide path switch (me_set_kernel_path): A/B tests and diagnostics.
@@ -944,6 +1283,9 @@ size_t mfma_ssd_scratch(const SearchArgs& p) {
 // SSD search; the caller routes partial rows / columns to the VALU kernels.
 static bool plan_mfma_ssd8(const SearchArgs& p, MfmaGeom* g);
 
+// Block-major (me_mfma_bm16_kernel) or 4x4-block tiles (me_mfma_ssd16_kernel)?
+static bool bm_auto(const SearchArgs& p) { return p.range <= 64; }
+
 bool plan_mfma_ssd(const SearchArgs& p, MfmaGeom* g) {
   if (p.cost_kind != COST_SSD) return false;
   if (p.blk == 8) return plan_mfma_ssd8(p, g);
@@ -952,9 +1294,17 @@ bool plan_mfma_ssd(const SearchArgs& p, MfmaGeom* g) {
   const int S = p.range, W = p.width, H = p.height;
   if (S < 1 || W < 16 || H < 16) return false;
   if (p.stride % 4 || (uintptr_t)p.cur % 4 || (uintptr_t)p.ref % 4) return false;
+  // block-major kernel for S <= 64 (ME_MFMA_BM=0|1: tuning override, read once)
+  static int force_bm = -1;
+  if (force_bm < 0) {
+    const char* e = getenv("ME_MFMA_BM");
+    force_bm = e ? (e[0] == '1' ? 1 : e[0] == '0' ? 0 : 2) : 2;
+  }
+  g->bm = S <= 64 && (force_bm == 1 || (force_bm == 2 && bm_auto(p)));
+  if (g->bm && p.stride % 16) g->bm = 0;  // 16-byte cur row loads
   const int nxmax = min(48 + 2 * S + 1, W - 15);
   const int ngx = (nxmax + 63) / 64;
-  if (ngx > 4) return false;  // S > 103: the VALU kernels take it
+  if (ngx > 4 && !g->bm) return false;  // S > 103: the VALU kernels take it
   const int nby = (H + 15) / 16;
   const int r0 = p.block_row_begin, r1 = p.block_row_end;
   g->row0 = r0;
@@ -994,10 +1344,12 @@ bool plan_mfma_ssd(const SearchArgs& p, MfmaGeom* g) {
     }
     if (force_w == 1 || force_w == 2) g->ngxw = force_w;
   }
-  if ((ngx + g->ngxw - 1) / g->ngxw > 1 &&
+  if (!g->bm && (ngx + g->ngxw - 1) / g->ngxw > 1 &&
       (!p.mkeys || !p.mcnt || p.merge_tiles < mfma_merge_tiles(p)))
     return false;  // tiles span workgroups: needs the merge buffers
   g->lds = 4 * (L + 15) * (64 * g->ngxw + 32) + 16 * 8 + 16 * 4 + L * 256 * g->ngxw;
+  g->bm_wpr = (g->nbx + 7) / 8;
+  if (g->bm) g->lds = BM_HDR + 2 * BM_WINB;
   g->mkeys = p.mkeys;
   g->mcnt = p.mcnt;
   g->ya0 = max(r0 * 16 - S, 0);
@@ -1042,6 +1394,7 @@ static bool plan_mfma_ssd8(const SearchArgs& p, MfmaGeom* g) {
   if (g->nrows <= 0) return false;
   g->hb = 8;
   g->hb_row = -1;
+  g->bm = 0;
   g->nbx = W / 8;
   g->tiles_x = (g->nbx + 3) / 4;
   g->tiles_y = (g->nrows + 3) / 4;
@@ -1092,6 +1445,16 @@ hipError_t launch_mfma_ssd(const SearchArgs& p, const MfmaGeom& g, hipStream_t s
       if (e != hipSuccess) return e;
     }
     hipLaunchKernelGGL(me_mfma_ssd8_kernel<4>, grid8, dim3(256), g.lds, stream, p, g);
+    return hipGetLastError();
+  }
+  if (g.bm) {
+    const dim3 gridb((unsigned)(g.nrows * g.bm_wpr));
+    if (g.lds > 64 * 1024) {
+      e = hipFuncSetAttribute((const void*)me_mfma_bm16_kernel,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, g.lds);
+      if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(me_mfma_bm16_kernel, gridb, dim3(256), g.lds, stream, p, g);
     return hipGetLastError();
   }
   const int wpt = (g.ngx + g.ngxw - 1) / g.ngxw;

@@ -109,6 +109,27 @@ __global__ void mfma_valu_mix(int iters, unsigned long long* out, int* sink) {
   sink[threadIdx.x] = c0[0] + c1[1] + c2[2] + c3[3] + (int)xs + (int)(f0[0] + f1[1] + f2[2] + f3[3]);
 }
 
+// 5. dependent chains: D accumulators (D = 1: every MFMA waits for the one
+//    before), 8 MFMAs per iteration, whole-workgroup span like 4.
+template <int D>
+__global__ void mfma_chain(int iters, unsigned long long* out, int* sink) {
+  const uint32_t h0 = 0x9E3779B9u * (threadIdx.x + 1);
+  v4i a = {(int)(h0 ^ 0x5bd1e995), (int)(h0 * 0x85ebca6b), (int)(h0 * 0xc2b2ae35), (int)(h0 + 0x27d4eb2f)};
+  v4i b = {(int)(h0 * 0x165667b1), (int)(h0 ^ 0xd3a2646c), (int)(h0 * 0xfd7046c5), (int)(h0 + 0xb55a4f09)};
+  v4i c[4] = {};
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  for (int i = 0; i < iters; i++) {
+#pragma unroll
+    for (int q = 0; q < 8; q++) c[q % D] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b, c[q % D], 0, 0, 0);
+  }
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+  if ((threadIdx.x & 63) == 0) {
+    out[1 + 2 * (threadIdx.x >> 6)] = t0;
+    out[2 + 2 * (threadIdx.x >> 6)] = t1;
+  }
+  sink[threadIdx.x] = c[0][0] + c[1 % 4][1] + c[2 % 4][2] + c[3][3];
+}
+
 __global__ void dma16_probe(const uint8_t* src, int nbytes, int shift, uint32_t* out) {
   __shared__ __align__(16) uint8_t lds[1024];
   const __amdgpu_buffer_rsrc_t rs =
@@ -242,6 +263,32 @@ int main() {
       run(mfma_valu_mix<0, 10>, "i8_16x16x64", 10, waves);
       run(mfma_valu_mix<0, 12>, "i8_16x16x64", 12, waves);
       run(mfma_valu_mix<0, 16>, "i8_16x16x64", 16, waves);
+    }
+  }
+  {
+    unsigned long long* dt2;
+    int* sink;
+    hipMalloc(&sink, 4096);
+    hipMalloc(&dt2, 8 * (1 + 2 * 16));
+    auto run = [&](auto kern, int d, int waves) {
+      const int iters = 10000;
+      unsigned long long tt[1 + 2 * 16];
+      for (int rep = 0; rep < 2; rep++) {
+        hipLaunchKernelGGL(kern, dim3(1), dim3(64 * waves), 0, 0, iters, dt2, sink);
+        hipMemcpy(tt, dt2, sizeof tt, hipMemcpyDeviceToHost);
+      }
+      unsigned long long lo = ~0ull, hi = 0;
+      for (int w = 0; w < waves; w++) {
+        lo = tt[1 + 2 * w] < lo ? tt[1 + 2 * w] : lo;
+        hi = tt[2 + 2 * w] > hi ? tt[2 + 2 * w] : hi;
+      }
+      printf("{\"probe\": \"mfma chain\", \"accumulators\": %d, \"waves_per_simd\": %d, \"simd_cycles_per_mfma\": %.2f}\n",
+             d, waves / 4, (double)(hi - lo) / iters / 8 / (waves / 4));
+    };
+    for (int waves : {4, 8, 16}) {
+      run(mfma_chain<1>, 1, waves);
+      run(mfma_chain<2>, 2, waves);
+      run(mfma_chain<4>, 4, waves);
     }
   }
   hipError_t e = hipDeviceSynchronize();
