@@ -1114,7 +1114,8 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_bm16_kernel(SearchArgs p, M
         const v4i s2c = __builtin_bit_cast(
             v4i, __builtin_amdgcn_raw_buffer_load_b128(rs2, s2v, srow + 64 * i, 0));
 #endif
-        const uint32_t lrow = lrow0 + (uint32_t)(16 * i);
+        // one base per tile, fragment rows at immediate offsets
+        const uint32_t lrow = (uint32_t)opaque((int)(lrow0 + (uint32_t)(16 * i)));
         v4i accA = zero4, accB = zero4;
         if constexpr (ma == 1 || ma == 2) accA = edge_mask(std::integral_constant<bool, ma == 2>{});
         if constexpr (mb == 1 || mb == 2) accB = edge_mask(std::integral_constant<bool, mb == 2>{});
