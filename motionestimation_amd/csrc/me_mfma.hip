@@ -253,6 +253,11 @@ __device__ __forceinline__ uint32_t sad_u32(uint32_t a_sgpr, uint32_t b, uint32_
   asm("v_sad_u32 %0, %1, %2, %3" : "=v"(d) : "s"(a_sgpr), "v"(b), "v"(c));
   return d;
 }
+__device__ __forceinline__ uint32_t umin3(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t d;
+  asm("v_min3_u32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
 __device__ __forceinline__ uint32_t lshl6_add(uint32_t a, uint32_t b_sgpr) {
   uint32_t d;
   asm("v_lshl_add_u32 %0, %1, 6, %2" : "=v"(d) : "v"(a), "s"(b_sgpr));
@@ -1073,17 +1078,13 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_bm16_kernel(SearchArgs p, M
   // same lanes for every such block: m < (bx - S) & 15, m > (bx + S) & 15.
   const bool fast = hasB && yover && bxA - S >= 0 && bxB + S <= W - 16 && i1A - i0A >= 2;
   const int mfa = (bxA - S) & 15, mlb = (bxA + S) & 15;
-  // built in the edge tiles (a few VALU there) rather than held in 8 VGPRs
-  auto edge_mask = [&](auto LAST) {
-    v4i mk;
-    const int m4 = opaque(4 * h);  // recomputed per use, not hoisted and spilled
+  v4i mF, mL;
 #pragma unroll
-    for (int r = 0; r < 4; r++) {
-      const int m = m4 + r;
-      mk[r] = (decltype(LAST)::value ? m > mlb : m < mfa) ? (1 << 24) : 0;
-    }
-    return mk;
-  };
+  for (int r = 0; r < 4; r++) {
+    const int m = 4 * h + r;
+    mF[r] = m < mfa ? (1 << 24) : 0;
+    mL[r] = m > mlb ? (1 << 24) : 0;
+  }
 
   const __amdgpu_buffer_rsrc_t rs2 =
       __builtin_amdgcn_make_buffer_rsrc((void*)g.s2, (short)0, g.s2_bytes, 0x00020000);
@@ -1116,9 +1117,8 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_bm16_kernel(SearchArgs p, M
 #endif
         // one base per tile, fragment rows at immediate offsets
         const uint32_t lrow = (uint32_t)opaque((int)(lrow0 + (uint32_t)(16 * i)));
-        v4i accA = zero4, accB = zero4;
-        if constexpr (ma == 1 || ma == 2) accA = edge_mask(std::integral_constant<bool, ma == 2>{});
-        if constexpr (mb == 1 || mb == 2) accB = edge_mask(std::integral_constant<bool, mb == 2>{});
+        v4i accA = ma == 1 ? mF : ma == 2 ? mL : zero4;
+        v4i accB = mb == 1 ? mF : mb == 2 ? mL : zero4;
         // Fragments in pairs, the next pair in flight during this pair's MFMAs
         // (four fragments live: the A fragments hold 64 VGPRs).
         auto ld = [&](int q) {
@@ -1172,8 +1172,8 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_bm16_kernel(SearchArgs p, M
 #pragma unroll
             for (int r = 0; r < 4; r++) k[r] |= ym;
           }
-          best = min(best, min(k[0], k[1]));
-          best = min(best, min(k[2], k[3]));
+          best = umin3(best, k[0], k[1]);
+          best = umin3(best, k[2], k[3]);
         };
         if constexpr (da) keys_of(accA, bA, i0A, i1A, 0, std::integral_constant<bool, ma == 3>{});
         if constexpr (db) keys_of(accB, bB, i0B, i1B, 2, std::integral_constant<bool, mb == 3>{});
