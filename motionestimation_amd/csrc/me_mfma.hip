@@ -94,114 +94,110 @@ __device__ __forceinline__ int opaque(int v) {
 //                 0 where the 16x16 window leaves the resident rows / frame
 //   s2h[rr][x]  = the same over hb rows (the partial bottom block row, block
 //                 height hb), rows >= s2h_row0 only (the last tile row's range)
-// One workgroup: 64 x 64 outputs from a 79 x 80 byte window in LDS.
-// Vertical sliding sums down each column into LDS (lanes on consecutive
-// columns: conflict-free), then horizontal sliding sums along each row in
-// registers, stored as 16 consecutive ints per thread.
-constexpr int PREP_W = 64 + 16;  // staged columns (64 + 15, dword padded)
-constexpr int PREP_R = 64 + 15;  // staged rows
+// One workgroup: 64 x 64 outputs, 320 threads = 80 columns (64 + 15 halo)
+// x 4 segments of 16 output rows.  Each thread loads its column's 15 + BH
+// rows straight from global memory (byte loads: a wave reads consecutive
+// bytes of a row, all loads of a thread independent), slides the BH-row sums
+// down them into LDS and stores its rp bytes; after one barrier, 256 threads
+// slide the BW-column sums along 16 outputs each.  (A staged 79 x 80 window in
+// LDS, then the same two passes, took twice as long: one more global-latency
+// phase and barrier per workgroup.)
+constexpr int PREP_W = 64 + 16;  // columns of vertical sums (64 + 15, padded)
 constexpr int VS_P = 84;         // ints per row of the vertical sums (16-byte rows, bank spread)
+constexpr int PREP_T = 4 * PREP_W;  // threads per workgroup
 
 __device__ __forceinline__ int sq127(int v) {
   v -= 127;
   return v * v;
 }
 
-// Vertical BH-row sums of one 16-row segment per task (every byte load
-// independent: one LDS latency per task), then horizontal 16-sums per
-// (row, 16 columns) in registers -> plane rows [row_lo, rows_alloc).
 template <int BH, int BW>
-__device__ __forceinline__ void box_pass(const MfmaGeom& g, const uint8_t* win, int* vs, int* plane,
-                                         int x0, int r0, int row_lo, int W) {
+__device__ __forceinline__ void prep_tile(const SearchArgs& p, const MfmaGeom& g, int* vs, int* plane,
+                                          int x0, int r0, int row_lo, bool write_rp) {
   const int tid = (int)threadIdx.x;
-  __syncthreads();  // vs free (a previous pass read it)
-  for (int t = tid; t < PREP_W * 4; t += 256) {  // (column, 16-row segment)
-    const int x = t % PREP_W, y0 = 16 * (t / PREP_W);
-    const uint8_t* c = win + y0 * PREP_W + x;
-    int q[16 + BH - 1];
+  const int W = p.width;
+  {
+    const int c = tid % PREP_W, y0 = 16 * (tid / PREP_W);
+    const int x = x0 + c;
+    const bool xin = x < W;
+    // frame row ya0 + rr; bytes outside the frame / resident rows read as 127
+    // (square term 0: they only feed outputs that are zeroed)
+    const uint8_t* col = p.ref + (ptrdiff_t)(g.ya0 - p.ref_row0) * p.stride + x;
+    int v[16 + BH - 1];
 #pragma unroll
-    for (int i = 0; i < 16 + BH - 1; i++) q[i] = (y0 + i < PREP_R) ? sq127(c[i * PREP_W]) : 0;
+    for (int i = 0; i < 16 + BH - 1; i++) {
+      const int rr = r0 + y0 + i;
+      v[i] = (xin && rr < g.rp_rows) ? (int)col[(ptrdiff_t)rr * p.stride] : 127;
+    }
     int s = 0;
 #pragma unroll
-    for (int i = 0; i < BH; i++) s += q[i];
+    for (int i = 0; i < BH; i++) s += sq127(v[i]);
 #pragma unroll
     for (int j = 0; j < 16; j++) {
-      vs[(y0 + j) * VS_P + x] = s;
-      if (j < 15) s += q[j + BH] - q[j];
+      vs[(y0 + j) * VS_P + c] = s;
+      if (j < 15) s += sq127(v[j + BH]) - sq127(v[j]);
+    }
+#if ME_MFMA_ABLATE & 16  // diagnostic: no rp stores
+    if (opaque(0))
+#endif
+    if (write_rp && c < 64 && x < g.pitch) {
+#pragma unroll
+      for (int j = 0; j < 16; j++) {
+        const int rr = r0 + y0 + j;
+        if (rr < g.rows_alloc)
+          __builtin_nontemporal_store((int8_t)((xin && rr < g.rp_rows) ? (v[j] ^ 0x80) : 0),
+                                      g.rp + (ptrdiff_t)rr * g.pitch + x);
+      }
     }
   }
   __syncthreads();
-  const int y = tid >> 2, xs = 16 * (tid & 3);
-  const int yy = r0 + y;
-  if (yy < g.rows_alloc && yy >= row_lo && x0 + xs < g.pitch) {
-    const int4* v4 = reinterpret_cast<const int4*>(vs + y * VS_P + xs);
-    int v[32];
+  // Horizontal sums, 4 outputs per task: consecutive lanes store consecutive
+  // 16-byte groups (a wave's store covers 1 KB of whole lines; 16-output tasks
+  // wrote 16 bytes per 64 and measured half the write bandwidth).
+  typedef int i32x4 __attribute__((ext_vector_type(4)));
+  for (int t = tid; t < 64 * 16; t += PREP_T) {
+    const int y = t >> 4, xs = 4 * (t & 15);
+    const int yy = r0 + y;
+    if (yy < g.rows_alloc && yy >= row_lo && x0 + xs < g.pitch) {
+      const i32x4* v4 = reinterpret_cast<const i32x4*>(vs + y * VS_P + xs);
+      int v[20];
 #pragma unroll
-    for (int k = 0; k < 8; k++) {
-      const int4 qq = v4[k];
-      v[4 * k] = qq.x; v[4 * k + 1] = qq.y; v[4 * k + 2] = qq.z; v[4 * k + 3] = qq.w;
-    }
-    int s = 0;
+      for (int k = 0; k < 5; k++) {
+        const i32x4 qq = v4[k];
+        v[4 * k] = qq[0]; v[4 * k + 1] = qq[1]; v[4 * k + 2] = qq[2]; v[4 * k + 3] = qq[3];
+      }
+      int sacc = 0;
 #pragma unroll
-    for (int j = 0; j < BW; j++) s += v[j];
-    const bool yok = yy <= g.rp_rows - BH;
-    int o[16];
+      for (int j = 0; j < BW; j++) sacc += v[j];
+      const bool yok = yy <= g.rp_rows - BH;
+      i32x4 o;
 #pragma unroll
-    for (int j = 0; j < 16; j++) {
-      o[j] = (yok && x0 + xs + j <= W - BW) ? s : 0;
-      s += v[j + BW] - v[j];
-    }
-    int4* dst = reinterpret_cast<int4*>(plane + (ptrdiff_t)yy * g.pitch + x0 + xs);
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      // non-temporal: the planes are read by the next kernel, not this one;
-      // nothing dirty is left in L2 for the end-of-kernel write-back
-      typedef int i32x4 __attribute__((ext_vector_type(4)));
-      const i32x4 v = {o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]};
-      __builtin_nontemporal_store(v, reinterpret_cast<i32x4*>(dst) + k);
+      for (int j = 0; j < 4; j++) {
+        o[j] = (yok && x0 + xs + j <= W - BW) ? sacc : 0;
+        if (j < 3) sacc += v[j + BW] - v[j];
+      }
+#if ME_MFMA_ABLATE & 8  // diagnostic: no s2 stores
+      if (o[0] == 0x7FFFFFF0 && o[3] == 3) plane[0] = o[1];
+      continue;
+#endif
+      // non-temporal: the planes are read by the next kernel, not this one
+      __builtin_nontemporal_store(o, reinterpret_cast<i32x4*>(plane + (ptrdiff_t)yy * g.pitch + x0 + xs));
     }
   }
 }
 
 template <int B>
-__global__ __launch_bounds__(256) void me_ssd_prep_kernel(SearchArgs p, MfmaGeom g) {
-  __shared__ __align__(16) uint8_t win[PREP_R * PREP_W];
+__global__ __launch_bounds__(PREP_T) void me_ssd_prep_kernel(SearchArgs p, MfmaGeom g) {
   __shared__ __align__(16) int vs[64 * VS_P];
-  const int tid = (int)threadIdx.x;
   // blockIdx.y < nmain: rp and s2 rows [64 y, +64); past it: s2h rows from s2h_row0
   const int nmain = (g.rows_alloc + 63) / 64;
   const bool hpass = (int)blockIdx.y >= nmain;
   const int x0 = (int)blockIdx.x * 64;
-  const int r0 = hpass ? g.s2h_row0 + 64 * ((int)blockIdx.y - nmain) : 64 * (int)blockIdx.y;
-  const int W = p.width;
-  const uint8_t* src = p.ref + (ptrdiff_t)(g.ya0 - p.ref_row0) * p.stride;
   PS_STAMP(0);
-  // stage; out-of-frame bytes = 127 (square term 0; they only feed zeroed outputs)
-  for (int i = tid; i < PREP_R * (PREP_W / 4); i += 256) {
-    const int rr = i / (PREP_W / 4), cw = i - rr * (PREP_W / 4);
-    const int y = r0 + rr, x = x0 + 4 * cw;
-    uint32_t v = 0x7F7F7F7Fu;
-    if (y < g.rp_rows) {
-      const uint8_t* row = src + (ptrdiff_t)y * p.stride;
-      if (x + 3 < W) {
-        v = *reinterpret_cast<const uint32_t*>(row + x);
-      } else {
-#pragma unroll
-        for (int b = 0; b < 4; b++)
-          if (x + b < W) v = (v & ~(0xFFu << (8 * b))) | ((uint32_t)row[x + b] << (8 * b));
-      }
-    }
-    reinterpret_cast<uint32_t*>(win)[i] = v;
-  }
-  __syncthreads();
-  PS_STAMP(1);
-#if ME_MFMA_ABLATE & 8  // diagnostic: prepass staging only
-  if (win[tid] == 0x5A && tid == 999) g.rp[0] = 1;
-  return;
-#endif
   if (hpass) {  // hb-row sums for the partial bottom block row's lanes
+    const int r0 = g.s2h_row0 + 64 * ((int)blockIdx.y - nmain);
     switch (g.hb) {
-#define ME_HB(k) case k: if constexpr (k < B) box_pass<k, B>(g, win, vs, g.s2h, x0, r0, g.s2h_row0, W); break;
+#define ME_HB(k) case k: if constexpr (k < B) prep_tile<k, B>(p, g, vs, g.s2h, x0, r0, g.s2h_row0, false); break;
       ME_HB(1) ME_HB(2) ME_HB(3) ME_HB(4) ME_HB(5) ME_HB(6) ME_HB(7) ME_HB(8)
       ME_HB(9) ME_HB(10) ME_HB(11) ME_HB(12) ME_HB(13) ME_HB(14) ME_HB(15)
 #undef ME_HB
@@ -209,21 +205,7 @@ __global__ __launch_bounds__(256) void me_ssd_prep_kernel(SearchArgs p, MfmaGeom
     }
     return;
   }
-  // rp: 64 x 64 bytes, one dword per thread per round
-  for (int i = tid; i < 64 * 16; i += 256) {
-    const int rr = i >> 4, cw = i & 15;
-    const int y = r0 + rr, x = x0 + 4 * cw;
-    if (y < g.rows_alloc && x < g.pitch) {
-      uint32_t v = reinterpret_cast<const uint32_t*>(win)[rr * (PREP_W / 4) + cw] ^ 0x80808080u;
-      if (y >= g.rp_rows) v = 0;
-      __builtin_nontemporal_store(v, reinterpret_cast<uint32_t*>(g.rp + (ptrdiff_t)y * g.pitch + x));
-    }
-  }
-#if ME_MFMA_ABLATE & 16  // diagnostic: prepass staging + rp only
-  return;
-#endif
-  PS_STAMP(2);
-  box_pass<B, B>(g, win, vs, g.s2, x0, r0, 0, W);
+  prep_tile<B, B>(p, g, vs, g.s2, x0, 64 * (int)blockIdx.y, 0, true);
   PS_STAMP(3);
 }
 
@@ -1433,9 +1415,9 @@ hipError_t launch_mfma_ssd(const SearchArgs& p, const MfmaGeom& g, hipStream_t s
   const int nh = g.hb_row >= 0 ? (g.rows_alloc - g.s2h_row0 + 63) / 64 : 0;
   dim3 pgrid((unsigned)((g.pitch + 63) / 64), (unsigned)(nmain + nh));
   if (p.blk == 8)
-    hipLaunchKernelGGL(me_ssd_prep_kernel<8>, pgrid, dim3(256), 0, stream, p, g);
+    hipLaunchKernelGGL(me_ssd_prep_kernel<8>, pgrid, dim3(PREP_T), 0, stream, p, g);
   else
-    hipLaunchKernelGGL(me_ssd_prep_kernel<16>, pgrid, dim3(256), 0, stream, p, g);
+    hipLaunchKernelGGL(me_ssd_prep_kernel<16>, pgrid, dim3(PREP_T), 0, stream, p, g);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   if (p.blk == 8) {
