@@ -111,9 +111,11 @@ __device__ __forceinline__ int sq127(int v) {
   return v * v;
 }
 
+constexpr int RPT_P = 80;  // bytes per row of the rp tile (16-byte aligned rows)
+
 template <int BH, int BW>
-__device__ __forceinline__ void prep_tile(const SearchArgs& p, const MfmaGeom& g, int* vs, int* plane,
-                                          int x0, int r0, int row_lo, bool write_rp) {
+__device__ __forceinline__ void prep_tile(const SearchArgs& p, const MfmaGeom& g, int* vs, uint8_t* rpt,
+                                          int* plane, int x0, int r0, int row_lo, bool write_rp) {
   const int tid = (int)threadIdx.x;
   const int W = p.width;
   {
@@ -137,20 +139,27 @@ __device__ __forceinline__ void prep_tile(const SearchArgs& p, const MfmaGeom& g
       vs[(y0 + j) * VS_P + c] = s;
       if (j < 15) s += sq127(v[j + BH]) - sq127(v[j]);
     }
-#if ME_MFMA_ABLATE & 16  // diagnostic: no rp stores
-    if (opaque(0))
-#endif
-    if (write_rp && c < 64 && x < g.pitch) {
+    if (write_rp && c < 64) {  // rp bytes via LDS: stored as whole 16-byte groups below
 #pragma unroll
       for (int j = 0; j < 16; j++) {
         const int rr = r0 + y0 + j;
-        if (rr < g.rows_alloc)
-          __builtin_nontemporal_store((int8_t)((xin && rr < g.rp_rows) ? (v[j] ^ 0x80) : 0),
-                                      g.rp + (ptrdiff_t)rr * g.pitch + x);
+        rpt[(y0 + j) * RPT_P + c] = (uint8_t)((xin && rr < g.rp_rows) ? (v[j] ^ 0x80) : 0);
       }
     }
   }
   __syncthreads();
+#if !(ME_MFMA_ABLATE & 16)  // diagnostic: no rp stores
+  if (write_rp) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    for (int t = tid; t < 64 * 4; t += PREP_T) {
+      const int y = t >> 2, xs = 16 * (t & 3);
+      const int rr = r0 + y;
+      if (rr < g.rows_alloc && x0 + xs < g.pitch)
+        __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(rpt + y * RPT_P + xs),
+                                    reinterpret_cast<u32x4*>(g.rp + (ptrdiff_t)rr * g.pitch + x0 + xs));
+    }
+  }
+#endif
   // Horizontal sums, 4 outputs per task: consecutive lanes store consecutive
   // 16-byte groups (a wave's store covers 1 KB of whole lines; 16-output tasks
   // wrote 16 bytes per 64 and measured half the write bandwidth).
@@ -181,7 +190,11 @@ __device__ __forceinline__ void prep_tile(const SearchArgs& p, const MfmaGeom& g
       continue;
 #endif
       // non-temporal: the planes are read by the next kernel, not this one
+#if ME_MFMA_ABLATE & 4096  // diagnostic: plain stores
+      *reinterpret_cast<i32x4*>(plane + (ptrdiff_t)yy * g.pitch + x0 + xs) = o;
+#else
       __builtin_nontemporal_store(o, reinterpret_cast<i32x4*>(plane + (ptrdiff_t)yy * g.pitch + x0 + xs));
+#endif
     }
   }
 }
@@ -189,6 +202,7 @@ __device__ __forceinline__ void prep_tile(const SearchArgs& p, const MfmaGeom& g
 template <int B>
 __global__ __launch_bounds__(PREP_T) void me_ssd_prep_kernel(SearchArgs p, MfmaGeom g) {
   __shared__ __align__(16) int vs[64 * VS_P];
+  __shared__ __align__(16) uint8_t rpt[64 * RPT_P];
   // blockIdx.y < nmain: rp and s2 rows [64 y, +64); past it: s2h rows from s2h_row0
   const int nmain = (g.rows_alloc + 63) / 64;
   const bool hpass = (int)blockIdx.y >= nmain;
@@ -197,7 +211,7 @@ __global__ __launch_bounds__(PREP_T) void me_ssd_prep_kernel(SearchArgs p, MfmaG
   if (hpass) {  // hb-row sums for the partial bottom block row's lanes
     const int r0 = g.s2h_row0 + 64 * ((int)blockIdx.y - nmain);
     switch (g.hb) {
-#define ME_HB(k) case k: if constexpr (k < B) prep_tile<k, B>(p, g, vs, g.s2h, x0, r0, g.s2h_row0, false); break;
+#define ME_HB(k) case k: if constexpr (k < B) prep_tile<k, B>(p, g, vs, rpt, g.s2h, x0, r0, g.s2h_row0, false); break;
       ME_HB(1) ME_HB(2) ME_HB(3) ME_HB(4) ME_HB(5) ME_HB(6) ME_HB(7) ME_HB(8)
       ME_HB(9) ME_HB(10) ME_HB(11) ME_HB(12) ME_HB(13) ME_HB(14) ME_HB(15)
 #undef ME_HB
@@ -205,7 +219,7 @@ __global__ __launch_bounds__(PREP_T) void me_ssd_prep_kernel(SearchArgs p, MfmaG
     }
     return;
   }
-  prep_tile<B, B>(p, g, vs, g.s2, x0, 64 * (int)blockIdx.y, 0, true);
+  prep_tile<B, B>(p, g, vs, rpt, g.s2, x0, 64 * (int)blockIdx.y, 0, true);
   PS_STAMP(3);
 }
 
