@@ -104,8 +104,11 @@ def cpu_baselines(ref, cur, blk, span, cost, threads, cands):
            "cpu_model": cpu_model, "host_cpus": os.cpu_count(),
            "sample": f"{what} {w}x{h} B{blk} +-{span} {cost.upper()} frame, "
                      f"oracle/me_oracle.c -O2, {threads} pthreads, median of 5 ({med*1e3:.1f} ms)"}
-    mes = os.path.join(REPO, "oracle", "_ref", "mes")
-    if os.path.exists(mes) and cost != "ssim":
+    # the reference binary at -O2, and as src/cpu/run.sh:4 builds it (-O0)
+    for key, name, opt in (("reference_binary", "mes", "-O2"), ("reference_binary_O0", "mes_O0", "-O0")):
+        mes = os.path.join(REPO, "oracle", "_ref", name)
+        if not os.path.exists(mes) or cost == "ssim":
+            continue
         with tempfile.TemporaryDirectory() as td:
             rp, cp = os.path.join(td, "ref.yuv"), os.path.join(td, "cur.yuv")
             ref.tofile(rp)
@@ -119,10 +122,10 @@ def cpu_baselines(ref, cur, blk, span, cost, threads, cands):
                         ms.append(float(line.split()[2]))
             if ms:
                 m = statistics.median(ms)
-                out["reference_binary"] = {
+                out[key] = {
                     "value": cands / (m / 1e3), "unit": "candidates/s", "cores": 100,
                     "kind": "reference", "cost": "mse",
-                    "sample": f"unmodified src/cpu (gcc -O2) on the same frame pair, its own "
+                    "sample": f"unmodified src/cpu (gcc {opt}) on the same frame pair, its own "
                               f"100-thread pool, 'Computation time' median of 3 ({m:.0f} ms)"}
     return out
 
