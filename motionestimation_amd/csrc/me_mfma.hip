@@ -70,6 +70,10 @@ __device__ __forceinline__ void sfor(F&& f) {
 // hw_id, xcc_id, realtime start, realtime end] (tools/mfma_stamps.py).
 __device__ unsigned long long g_mstamps[8 << 14];
 #define MS_STAMP(slot, v) do { if (threadIdx.x == 0 && blockIdx.x < (1u << 14)) g_mstamps[8 * blockIdx.x + (slot)] = (v); } while (0)
+// block-major kernel: per workgroup and band, [wave 0 compute done, barrier passed]
+__device__ unsigned long long g_bstamps[32 << 12];
+#define BS_STAMP(slot) do { if (threadIdx.x == 0 && blockIdx.x < (1u << 12) && (slot) < 32) \
+  g_bstamps[32 * blockIdx.x + (slot)] = __builtin_amdgcn_s_memtime(); } while (0)
 // prepass: [start, staged, rp done, end] per workgroup, after the main kernel's slots
 __device__ unsigned long long g_pstamps[6 << 14];
 #define PS_STAMP(slot) do { const unsigned b_ = blockIdx.y * gridDim.x + blockIdx.x; \
@@ -77,6 +81,7 @@ __device__ unsigned long long g_pstamps[6 << 14];
     if ((slot) == 0 || (slot) == 3) g_pstamps[6 * b_ + 4 + ((slot) == 3)] = __builtin_amdgcn_s_memrealtime(); } } while (0)
 #else
 #define MS_STAMP(slot, v) do { } while (0)
+#define BS_STAMP(slot) do { } while (0)
 #define PS_STAMP(slot) do { } while (0)
 #endif
 
@@ -1203,8 +1208,10 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_bm16_kernel(SearchArgs p, M
       bestB = (kB >> 32) < (bestB >> 32) ? kB : bestB;
     }
     if (s == 0) MS_STAMP(2, __builtin_amdgcn_s_memtime());
+    BS_STAMP(2 * s);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // band s + 1 landed (this thread's pieces)
     __syncthreads();                                   // ... and everyone's; band s free
+    BS_STAMP(2 * s + 1);
   }
   if (hasA) {
     auto emit = [&](unsigned long long b, int j, int ccj, int bx) {
@@ -1477,6 +1484,11 @@ hipError_t launch_mfma_ssd(const SearchArgs& p, const MfmaGeom& g, hipStream_t s
 extern "C" int me_debug_prep_stamps(unsigned long long* out, int n_words) {
   if (n_words > (6 << 14)) n_words = 6 << 14;
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(me::g_pstamps), (size_t)n_words * 8, 0,
+                                  hipMemcpyDeviceToHost);
+}
+extern "C" int me_debug_band_stamps(unsigned long long* out, int n_words) {
+  if (n_words > (32 << 12)) n_words = 32 << 12;
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(me::g_bstamps), (size_t)n_words * 8, 0,
                                   hipMemcpyDeviceToHost);
 }
 extern "C" int me_debug_mfma_stamps(unsigned long long* out, int n_words) {

@@ -60,15 +60,14 @@ for i in range(len(ucu)):
     conc.append(m)
 print(f"  max concurrent WGs per CU: histogram {np.bincount(conc)[1:]}")
 
-# prepass phases (s_memtime per workgroup): staging, rp, box sums
+# prepass lifetimes (s_memtime per workgroup: start, end)
 L.me_debug_prep_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
 pb = np.zeros(6 << 14, np.uint64)
 L.me_debug_prep_stamps(pb.ctypes.data, pb.size)
 ps = pb.reshape(-1, 6)
 full = ps[(ps[:, 3] > 0)].astype(np.float64)
-print(f"prepass: {len(full)} main workgroups; cycles median: stage {np.median(full[:, 1] - full[:, 0]):.0f}, "
-      f"rp {np.median(full[:, 2] - full[:, 1]):.0f}, box {np.median(full[:, 3] - full[:, 2]):.0f}; "
-      f"lifetime max {np.max(full[:, 3] - full[:, 0]):.0f}")
+print(f"prepass: {len(full)} main workgroups; lifetime cycles median {np.median(full[:, 3] - full[:, 0]):.0f}, "
+      f"max {np.max(full[:, 3] - full[:, 0]):.0f}")
 ra, rb = full[:, 4] - full[:, 4].min(), full[:, 5] - full[:, 4].min()
 print(f"prepass realtime us: starts min {ra.min()/100:.2f} median {np.median(ra)/100:.2f} max {ra.max()/100:.2f}; "
       f"ends max {rb.max()/100:.2f}")
@@ -77,3 +76,25 @@ ids = np.nonzero(buf.reshape(-1, 8)[:, 3] > 0)[0]
 life = b - a
 order = np.argsort(-life)[:12]
 print("  slowest WGs (blockIdx, lifetime us):", [(int(ids[i]), round(float(life[i]), 1)) for i in order])
+
+# block-major kernel: per band, wave 0's compute end and the barrier exit
+try:
+    L.me_debug_band_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    bs = np.zeros(32 << 12, np.uint64)
+    L.me_debug_band_stamps(bs.ctypes.data, bs.size)
+    bs = bs.reshape(-1, 32).astype(np.float64)
+    mst = buf.reshape(-1, 8).astype(np.float64)
+    rows = []
+    for w in range(min(len(bs), len(mst))):
+        if mst[w, 1] == 0 or bs[w, 0] == 0:
+            continue
+        t = [mst[w, 1]] + [v for v in bs[w] if v > 0]
+        rows.append(np.diff(np.array(t)))
+    if rows:
+        n = max(len(r) for r in rows)
+        full = [r for r in rows if len(r) == n]
+        med = np.median(np.array(full), axis=0)
+        print(f"bands: {len(full)} workgroups with {n // 2} bands; median cycles per band "
+              f"[compute, barrier wait]: " + ", ".join(f"[{med[2*i]:.0f}, {med[2*i+1]:.0f}]" for i in range(n // 2)))
+except AttributeError:
+    pass
