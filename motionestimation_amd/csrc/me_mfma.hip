@@ -1305,7 +1305,7 @@ bool plan_mfma_ssd(const SearchArgs& p, MfmaGeom* g) {
     force_bm = e ? (e[0] == '1' ? 1 : e[0] == '0' ? 0 : 2) : 2;
   }
   g->bm = S <= 64 && (force_bm == 1 || (force_bm == 2 && bm_auto(p)));
-  if (g->bm && p.stride % 16) g->bm = 0;  // 16-byte cur row loads
+  if (g->bm && (p.stride % 16 || (uintptr_t)p.cur % 16)) g->bm = 0;  // 16-byte cur row loads
   const int nxmax = min(48 + 2 * S + 1, W - 15);
   const int ngx = (nxmax + 63) / 64;
   if (ngx > 4 && !g->bm) return false;  // S > 103: the VALU kernels take it
