@@ -1,6 +1,6 @@
 // me_mfma.hip -- the reference's cost (float MSE = SSD / (w*h), souravBhat/
 // MotionEstimation src/cpu/main.c:18-36) on the CDNA4 matrix cores, for 16x16
-// blocks.  SAD stays on the VALU (|a - b| is no contraction); SSD is one:
+// and 8x8 blocks.  SAD stays on the VALU (|a - b| is no contraction); SSD is one:
 //
 //   SSD(block m, candidate top-left (x, y))
 //     = sum (c - r)^2 = Cc_m + S2(x, y) + 2 X_m(x, y)
@@ -12,7 +12,13 @@
 // main.c:53-60) and the reported SSD are the VALU kernels' bit for bit, and
 // through them the reference's float-MSE choice.
 //
-// GEMM shape: M = 16 blocks of a 4x4 block tile, N = 16 candidate positions,
+// Three kernels share this decomposition and the prepass (plan_mfma_ssd picks):
+//   me_mfma_bm16_kernel   16x16, S <= 64: block-major GEMMs (one block per
+//                         output tile, see its comment) -- the default path
+//   me_mfma_ssd16_kernel  16x16, 64 < S <= 103: 4x4-block tiles (below)
+//   me_mfma_ssd8_kernel   8x8: one MFMA per 4x4-block tile and position row
+//
+// 4x4-block tiles: M = 16 blocks of a 4x4 block tile, N = 16 candidate positions,
 // K = 64 = 4 block rows x 16 columns; four MFMAs (q = 0..3, block rows 4q..4q+3)
 // complete one 16x16 output tile (16 positions at one y, 16 blocks).  The B
 // operand of lane (n, h) is window row R + h at position x_n, and it feeds
