@@ -1368,7 +1368,9 @@ bool plan_mfma_ssd(const SearchArgs& p, MfmaGeom* g) {
   g->pitch = (W + 15) & ~15;
   // + 80 rows of slack: the last chunk of a tile reads (masked) window rows and
   // S2 entries up to L + 15 rows past the planes' last row.
-  g->rows_alloc = g->rp_rows + 80;
+  // (the block-major kernel reads at most 15 rows past them, and its buffer
+  // loads are range-checked: 16 rows of slack)
+  g->rows_alloc = g->rp_rows + (g->bm ? 16 : 80);
   // the last tile row's candidate rows start here (its lanes of the partial
   // block row read s2h from there on)
   const int tly_last = 16 * (r0 + 4 * (g->tiles_y - 1));
