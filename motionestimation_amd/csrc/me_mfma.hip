@@ -864,7 +864,7 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd8_kernel(SearchArgs p, M
           uint32_t kc[4];
           keys_of(t, acc, sv[t & 1], kc, MASKED);
 #pragma unroll
-          for (int r = 0; r < 4; r++) best[r] = min(best[r], min(kp[r], kc[r]));
+          for (int r = 0; r < 4; r++) best[r] = umin3(best[r], kp[r], kc[r]);
         }
       });
     };
