@@ -173,3 +173,27 @@ def test_mfma8_8k_s128_sampled(engine):
         omv, ocost, _ = O.full_search(ref, cur, 8, 128, "ssd", threads=NT, begin=b0, end=b1)
         np.testing.assert_array_equal(mv[b0:b1], omv, err_msg=f"row {row}")
         np.testing.assert_array_equal(cost[b0:b1], ocost)
+
+
+# ------------------------------------------------------------------ fuzz
+def test_mfma_random_shapes(engine):
+    """Seeded random frame sizes, ranges and block sizes on every MFMA kernel
+    (block-major, 4x4-block tiles, 8x8) and their edge paths, against the
+    oracle: widths/heights not multiples of B, ranges from 1 to 103, noise and
+    smooth content."""
+    rng = np.random.default_rng(4242)
+    for it in range(150):
+        blk = int(rng.choice([8, 16]))
+        span = int(rng.integers(1, 104 if blk == 16 else 80))
+        h = int(rng.integers(blk, 200))
+        w = int(rng.integers(blk, 260))
+        if rng.random() < 0.5:
+            ref = rng.integers(0, 256, (h, w), dtype=np.uint8)
+            cur = rng.integers(0, 256, (h, w), dtype=np.uint8)
+        else:
+            ref, cur = _pair(rng, h, w, dx=int(rng.integers(-4, 5)), dy=int(rng.integers(-4, 5)))
+        mv, cost = engine.full_search(ref, cur, blk, span, "ssd")
+        omv, ocost, _ = O.full_search(ref, cur, blk, span, "ssd", threads=NT)
+        tag = f"it{it} {h}x{w} B{blk} S{span}"
+        np.testing.assert_array_equal(mv, omv, err_msg=tag)
+        np.testing.assert_array_equal(cost, ocost, err_msg=tag)
