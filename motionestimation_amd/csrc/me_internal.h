@@ -42,6 +42,7 @@ struct Dev {
   uint8_t* stage[2] = {nullptr, nullptr};  // pinned staging for pageable frames
   hipEvent_t stage_ev[2] = {nullptr, nullptr};
   size_t stage_bytes = 0;
+  hipEvent_t pair_ev[8] = {};  // search of pair n done: bounds how far the host runs ahead
   uint8_t* pair_out = nullptr;  // [pairs][nblocks] mv records, then [pairs][nblocks] costs
   size_t pair_out_cap = 0;
 };

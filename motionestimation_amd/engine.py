@@ -188,7 +188,10 @@ class _Pinned:
 
     def __del__(self):
         if getattr(self, "ptr", None):
-            _lib.lib().me_host_free(self.ptr)
+            try:
+                _lib.lib().me_host_free(self.ptr)
+            except Exception:  # interpreter shutdown: module globals already torn down
+                pass
             self.ptr = None
 
 

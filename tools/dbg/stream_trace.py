@@ -1,0 +1,21 @@
+"""Streaming leg alone (bench.host_stream's pinned case) for a rocprofv3 timeline."""
+import os, sys, time
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+import numpy as np
+import torch
+import motionestimation_amd as me
+from motionestimation_amd import synth
+
+w, h, npairs = 1920, 1080, int(sys.argv[1]) if len(sys.argv) > 1 else 16
+eng = me.Engine(devices=[0])
+pinned = me.pinned_frames(npairs + 1, h, w)
+synth.sequence(w, h, npairs + 1, 1, 3, -3, out=pinned)
+pairs = [(k, k + 1) for k in range(npairs)]
+frames = list(pinned)
+eng.search_pairs(frames, pairs, 16, 32, "sad")
+torch.cuda.synchronize()
+for rep in range(3):
+    t0 = time.perf_counter()
+    eng.search_pairs(frames, pairs, 16, 32, "sad")
+    dt = time.perf_counter() - t0
+    print(f"{npairs} pairs: {dt*1e3:.3f} ms, {npairs/dt:.0f} pairs/s", flush=True)
