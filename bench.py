@@ -137,7 +137,7 @@ def host_stream(eng, w, h, blk, span, cost, seed, sx, sy, kern_ms, cands_frame):
     Reported beside `value`, never as it: `value` has the inputs in HBM."""
     import motionestimation_amd as me
     from motionestimation_amd import synth
-    npairs = 16 if w * h <= 2_100_000 else (8 if w * h <= 8_300_000 else 4)
+    npairs = 64 if w * h <= 2_100_000 else (16 if w * h <= 8_300_000 else 4)
     pinned = me.pinned_frames(npairs + 1, h, w)
     synth.sequence(w, h, npairs + 1, seed, sx, sy, out=pinned)
     pageable = np.array(pinned)
