@@ -13,9 +13,9 @@
 // through them the reference's float-MSE choice.
 //
 // Three kernels share this decomposition and the prepass (plan_mfma_ssd picks):
-//   me_mfma_bm16_kernel   16x16, S <= 64: block-major GEMMs (one block per
-//                         output tile, see its comment) -- the default path
-//   me_mfma_ssd16_kernel  16x16, 64 < S <= 103: 4x4-block tiles (below)
+//   me_mfma_bm16_kernel   16x16: block-major GEMMs (one block per output
+//                         tile, see its comment) -- the default path
+//   me_mfma_ssd16_kernel  16x16, S <= 103, unaligned rows: 4x4-block tiles (below)
 //   me_mfma_ssd8_kernel   8x8: one MFMA per 4x4-block tile and position row
 //
 // 4x4-block tiles: M = 16 blocks of a 4x4 block tile, N = 16 candidate positions,
@@ -949,13 +949,17 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd8_kernel(SearchArgs p, M
 // the range's last row (overlapping its predecessor), so no y mask.  Per band
 // the lane's best is widened to (key >> 6, s << 6 | idx), which orders by SSD,
 // then dy, then dx (the raster-first rule); the lanes meet in a 64-bit LDS min.
-constexpr int BM_LP = 288;    // window row pitch (16-byte slots 2n + (h & 1) mod 16: conflict-free b128)
+// Window row pitch LP = 288 (S <= 64) or 544 (S <= 103): LP = 32 (mod 256) puts
+// the 16-byte slots 2n + (h & 1) (mod 16) of a ds_read_b128 lane group on
+// distinct banks.
 constexpr int BM_CREC = 48;   // cur row record: 16 zero bytes, the row (c ^ 0x7F), 16 zero bytes
 constexpr int BM_HDR = 8 * 16 * BM_CREC + 8 * 8 + 8 * 4;  // records, keys, cc
-constexpr int BM_WINB = 31 * BM_LP;  // one band's window rows
 
+template <int LP>
 __global__ __launch_bounds__(256)
 __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_bm16_kernel(SearchArgs p, MfmaGeom g) {
+  constexpr int BM_LP = LP;
+  constexpr int BM_WINB = 31 * LP;  // one band's window rows
   extern __shared__ __align__(16) uint8_t smem[];
   uint8_t* crec = smem;
   unsigned long long* keys = reinterpret_cast<unsigned long long*>(smem + 8 * 16 * BM_CREC);
@@ -1294,7 +1298,9 @@ size_t mfma_ssd_scratch(const SearchArgs& p) {
 static bool plan_mfma_ssd8(const SearchArgs& p, MfmaGeom* g);
 
 // Block-major (me_mfma_bm16_kernel) or 4x4-block tiles (me_mfma_ssd16_kernel)?
-static bool bm_auto(const SearchArgs& p) { return p.range <= 64; }
+// Block-major measured faster at every S (1080p, S = 2..103: tools/dbg/bm_sweep*.sh);
+// the tile kernel remains for row pitches / cur pointers that are not 16-byte aligned.
+static bool bm_auto(const SearchArgs& p) { return p.range <= 103; }
 
 bool plan_mfma_ssd(const SearchArgs& p, MfmaGeom* g) {
   if (p.cost_kind != COST_SSD) return false;
@@ -1304,13 +1310,15 @@ bool plan_mfma_ssd(const SearchArgs& p, MfmaGeom* g) {
   const int S = p.range, W = p.width, H = p.height;
   if (S < 1 || W < 16 || H < 16) return false;
   if (p.stride % 4 || (uintptr_t)p.cur % 4 || (uintptr_t)p.ref % 4) return false;
-  // block-major kernel for S <= 64 (ME_MFMA_BM=0|1: tuning override, read once)
+  // block-major kernel for S <= 103 (ME_MFMA_BM=0|1: tuning override, read once)
   static int force_bm = -1;
   if (force_bm < 0) {
     const char* e = getenv("ME_MFMA_BM");
     force_bm = e ? (e[0] == '1' ? 1 : e[0] == '0' ? 0 : 2) : 2;
   }
-  g->bm = S <= 64 && (force_bm == 1 || (force_bm == 2 && bm_auto(p)));
+  g->bm = S <= 103 && (force_bm == 1 || (force_bm == 2 && bm_auto(p)));
+  // window row pitch: a workgroup's 8 blocks span 16 (tc1 - tc0) + 32 <= 16 (S / 8 + 8) + 32 bytes
+  g->bm_lp = S <= 64 ? 288 : 544;
   if (g->bm && (p.stride % 16 || (uintptr_t)p.cur % 16)) g->bm = 0;  // 16-byte cur row loads
   const int nxmax = min(48 + 2 * S + 1, W - 15);
   const int ngx = (nxmax + 63) / 64;
@@ -1359,7 +1367,7 @@ bool plan_mfma_ssd(const SearchArgs& p, MfmaGeom* g) {
     return false;  // tiles span workgroups: needs the merge buffers
   g->lds = 4 * (L + 15) * (64 * g->ngxw + 32) + 16 * 8 + 16 * 4 + L * 256 * g->ngxw;
   g->bm_wpr = (g->nbx + 7) / 8;
-  if (g->bm) g->lds = BM_HDR + 2 * BM_WINB;
+  if (g->bm) g->lds = BM_HDR + 2 * 31 * g->bm_lp;
   g->mkeys = p.mkeys;
   g->mcnt = p.mcnt;
   g->ya0 = max(r0 * 16 - S, 0);
@@ -1461,12 +1469,10 @@ hipError_t launch_mfma_ssd(const SearchArgs& p, const MfmaGeom& g, hipStream_t s
   }
   if (g.bm) {
     const dim3 gridb((unsigned)(g.nrows * g.bm_wpr));
-    if (g.lds > 64 * 1024) {
-      e = hipFuncSetAttribute((const void*)me_mfma_bm16_kernel,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, g.lds);
-      if (e != hipSuccess) return e;
-    }
-    hipLaunchKernelGGL(me_mfma_bm16_kernel, gridb, dim3(256), g.lds, stream, p, g);
+    if (g.bm_lp == 288)
+      hipLaunchKernelGGL(me_mfma_bm16_kernel<288>, gridb, dim3(256), g.lds, stream, p, g);
+    else
+      hipLaunchKernelGGL(me_mfma_bm16_kernel<544>, gridb, dim3(256), g.lds, stream, p, g);
     return hipGetLastError();
   }
   const int wpt = (g.ngx + g.ngxw - 1) / g.ngxw;
