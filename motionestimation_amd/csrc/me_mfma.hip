@@ -52,6 +52,9 @@
 #ifndef ME_MFMA_DLY
 #define ME_MFMA_DLY 1  // 1..3 (the 16-register accumulator ring holds 13 + DLY rows)
 #endif
+#ifndef ME_SSD8_WP
+#define ME_SSD8_WP 80  // 8x8 window copy pitch: 4 x 72 x 80 + S2 table = 40 KB, four workgroups per CU
+#endif
 #ifndef ME_MFMA_ABLATE
 #define ME_MFMA_ABLATE 0  // diagnostic bit set (csrc/Makefile mablate, tools/mablate.sh); never shipped
 #endif
@@ -662,7 +665,7 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd16_kernel(SearchArgs p, 
 template <int KM8>
 __global__ __launch_bounds__(256)
 __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd8_kernel(SearchArgs p, MfmaGeom g) {
-  constexpr int WP = 64 + 32;      // bytes per copy row (64 positions + 7 + align)
+  constexpr int WP = ME_SSD8_WP;   // bytes per copy row (64 positions + 7 + align, 16-byte granules)
   constexpr int L = 16 * KM8;      // candidate rows per chunk (yidx < 64)
   constexpr int CROWS = L + 8;     // rows y0 .. y0 + L + 6, + the last (unused) prefetch
   constexpr int COPY = CROWS * WP;
@@ -1424,7 +1427,7 @@ static bool plan_mfma_ssd8(const SearchArgs& p, MfmaGeom* g) {
   if (g->ngx > 1 && (!p.mkeys || !p.mcnt || p.merge_tiles < mfma_merge_tiles(p))) return false;
   g->km = 4;  // L = 64
   const int L = 16 * g->km;
-  g->lds = 4 * (L + 8) * 96 + 16 * 8 + 16 * 4 + (L + 1) * 256;
+  g->lds = 4 * (L + 8) * ME_SSD8_WP + 16 * 8 + 16 * 4 + (L + 1) * 256;
   g->ya0 = max(r0 * 8 - S, 0);
   const int ya1 = min(r1 * 8 + S, H);
   g->rp_rows = ya1 - g->ya0;
