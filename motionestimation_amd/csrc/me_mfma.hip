@@ -15,7 +15,7 @@
 // Three kernels share this decomposition and the prepass (plan_mfma_ssd picks):
 //   me_mfma_bm16_kernel   16x16: block-major GEMMs (one block per output
 //                         tile, see its comment) -- the default path
-//   me_mfma_ssd16_kernel  16x16, S <= 103, unaligned rows: 4x4-block tiles (below)
+//   me_mfma_ssd16_kernel  16x16, S <= 103, rows not 16-byte aligned: 4x4-block tiles
 //   me_mfma_ssd8_kernel   8x8: one MFMA per 4x4-block tile and position row
 //
 // 4x4-block tiles: M = 16 blocks of a 4x4 block tile, N = 16 candidate positions,
@@ -943,8 +943,8 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd8_kernel(SearchArgs p, M
 // window (rows [ylo, ylo + 16 Ty + 15), 16-aligned columns) is DMA'd once:
 // no chunks, no cross-workgroup merge.
 //   lane (n, h), result r: position x = 16 i + 4 h + r, y = Ys + n
-//   key = ((2 X + S2 + 1 + 2^23) << 6) + 4 (i - iu0) + r
-//       = (X << 7) + ((S2 << 6) + 2^29 + 64 + 4 (i - iu0) + r)
+//   key = ((2 X + S2 + 1 + 2^23) << 6) + 4 ((i - iu0) & 15) + r
+//       = (X << 7) + ((S2 << 6) + 2^29 + 64 + 4 ((i - iu0) & 15) + r)
 // 2 X + S2 = SSD - Cc with Cc <= 2^22, so valid keys lie in (0, 2^31), and any
 // window content keeps 2 X + S2 + 1 + 2^23 in (0, 2^25): positions outside
 // the block's x range get 2^24 added to the accumulator (key + 2^31, first and
@@ -952,7 +952,7 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd8_kernel(SearchArgs p, M
 // the range's last row (overlapping its predecessor), so no y mask.  Per band
 // the lane's best is widened to (key >> 6, s << 6 | idx), which orders by SSD,
 // then dy, then dx (the raster-first rule); the lanes meet in a 64-bit LDS min.
-// Window row pitch LP = 288 (S <= 64) or 544 (S <= 103): LP = 32 (mod 256) puts
+// Window row pitch LP = 288 (S <= 64) or 544 (S <= 192): LP = 32 (mod 256) puts
 // the 16-byte slots 2n + (h & 1) (mod 16) of a ds_read_b128 lane group on
 // distinct banks.
 constexpr int BM_CREC = 48;   // cur row record: 16 zero bytes, the row (c ^ 0x7F), 16 zero bytes
@@ -1116,6 +1116,19 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_bm16_kernel(SearchArgs p, M
       const uint32_t lrow0 = lbase + (uint32_t)((s & 1) * BM_WINB);
       const int srow = (Ys - g.ya0) * g.pitch * 4;
       uint32_t bA = ~0u, bB = ~0u;
+      // Widen the lane's 32-bit bests to (key >> 6, band << 8 | segment << 6 | idx):
+      // a key's 6-bit index holds 16 tiles, so every 16 tiles of a band form a
+      // segment.  The strictly better key wins: an earlier band (smaller dy) or
+      // segment (smaller dx) keeps ties.
+      auto widen = [&](int seg) {
+        const uint32_t lo = ((uint32_t)s << 8) | ((uint32_t)seg << 6);
+        const unsigned long long kA = ((unsigned long long)(bA >> 6) << 32) | lo | (bA & 63u);
+        const unsigned long long kB = ((unsigned long long)(bB >> 6) << 32) | lo | (bB & 63u);
+        bestA = (kA >> 32) < (bestA >> 32) ? kA : bestA;
+        bestB = (kB >> 32) < (bestB >> 32) ? kB : bestB;
+        bA = ~0u;
+        bB = ~0u;
+      };
       // One 16 x 16 output tile per block at window column 16 i.  MA / MB: the
       // mask of block A / B on this tile -- 0 none, 1 the first-tile mask mF, 2
       // the last-tile mask mL (both as the first MFMA's accumulator input, no
@@ -1159,9 +1172,10 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_bm16_kernel(SearchArgs p, M
           f0 = n0;
           f1 = n1;
         }
-        // key = ((2 acc + S2 + 1 + 2^23) << 6) + 4 (i - iu0) + r, acc = X (+ masks):
+        // key = ((2 acc + S2 + 1 + 2^23) << 6) + 4 ((i - iu0) & 15) + r, acc = X (+ masks):
         // one v_lshl_add for the shared position term, one per key
-        const uint32_t kb = (1u << 29) + 64u + 4u * (uint32_t)(i - iu0);
+        const int rel = i - iu0;
+        const uint32_t kb = (1u << 29) + 64u + 4u * (uint32_t)(rel & 15);
         uint32_t P[4];
 #pragma unroll
         for (int r = 0; r < 4; r++) P[r] = lshl6_add((uint32_t)s2c[r], kb + (uint32_t)r);
@@ -1191,6 +1205,7 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_bm16_kernel(SearchArgs p, M
         };
         if constexpr (da) keys_of(accA, bA, i0A, i1A, 0, std::integral_constant<bool, ma == 3>{});
         if constexpr (db) keys_of(accB, bB, i0B, i1B, 2, std::integral_constant<bool, mb == 3>{});
+        if ((rel & 15) == 15 && i < iu1) widen(rel >> 4);  // S > 56: a band spans > 16 tiles
       };
       using T_ = std::true_type;
       using F_ = std::false_type;
@@ -1213,12 +1228,7 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_bm16_kernel(SearchArgs p, M
           else tile(i, F_{}, T_{}, M3{}, M3{});
         }
       }
-      // end of the band: widen; the strictly better key wins (an earlier band, a
-      // smaller dy, keeps ties)
-      const unsigned long long kA = ((unsigned long long)(bA >> 6) << 32) | ((uint32_t)s << 6) | (bA & 63u);
-      const unsigned long long kB = ((unsigned long long)(bB >> 6) << 32) | ((uint32_t)s << 6) | (bB & 63u);
-      bestA = (kA >> 32) < (bestA >> 32) ? kA : bestA;
-      bestB = (kB >> 32) < (bestB >> 32) ? kB : bestB;
+      widen((iu1 - iu0) >> 4);  // end of the band
     }
     if (s == 0) MS_STAMP(2, __builtin_amdgcn_s_memtime());
     BS_STAMP(2 * s);
@@ -1231,9 +1241,9 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_bm16_kernel(SearchArgs p, M
       const uint32_t hi = (uint32_t)(b >> 32);
       if (hi < (1u << 25)) {
         const uint32_t lo = (uint32_t)b;
-        const int sb = (int)(lo >> 6), idx = (int)(lo & 63u);
+        const int sb = (int)(lo >> 8), seg = (int)((lo >> 6) & 3u), idx = (int)(lo & 63u);
         const uint32_t cost = hi - 1u - (1u << 23) + (uint32_t)ccj;
-        const int dx = 16 * (iu0 + (idx >> 2)) + 4 * h + (idx & 3) - bx;
+        const int dx = 16 * (iu0 + 16 * seg + (idx >> 2)) + 4 * h + (idx & 3) - bx;
         const int dy = band_y(sb) + n - by;
         const unsigned long long key = ((unsigned long long)cost << 32) |
                                        ((uint32_t)(dy + 32768) << 16) | (uint32_t)(dx + 32768);
@@ -1303,7 +1313,7 @@ static bool plan_mfma_ssd8(const SearchArgs& p, MfmaGeom* g);
 // Block-major (me_mfma_bm16_kernel) or 4x4-block tiles (me_mfma_ssd16_kernel)?
 // Block-major measured faster at every S (1080p, S = 2..103: tools/dbg/bm_sweep*.sh);
 // the tile kernel remains for row pitches / cur pointers that are not 16-byte aligned.
-static bool bm_auto(const SearchArgs& p) { return p.range <= 103; }
+static bool bm_auto(const SearchArgs& p) { return p.range <= 192; }
 
 bool plan_mfma_ssd(const SearchArgs& p, MfmaGeom* g) {
   if (p.cost_kind != COST_SSD) return false;
@@ -1313,14 +1323,15 @@ bool plan_mfma_ssd(const SearchArgs& p, MfmaGeom* g) {
   const int S = p.range, W = p.width, H = p.height;
   if (S < 1 || W < 16 || H < 16) return false;
   if (p.stride % 4 || (uintptr_t)p.cur % 4 || (uintptr_t)p.ref % 4) return false;
-  // block-major kernel for S <= 103 (ME_MFMA_BM=0|1: tuning override, read once)
+  // block-major kernel for S <= 192 (ME_MFMA_BM=0|1: tuning override, read once)
   static int force_bm = -1;
   if (force_bm < 0) {
     const char* e = getenv("ME_MFMA_BM");
     force_bm = e ? (e[0] == '1' ? 1 : e[0] == '0' ? 0 : 2) : 2;
   }
-  g->bm = S <= 103 && (force_bm == 1 || (force_bm == 2 && bm_auto(p)));
-  // window row pitch: a workgroup's 8 blocks span 16 (tc1 - tc0) + 32 <= 16 (S / 8 + 8) + 32 bytes
+  g->bm = S <= 192 && (force_bm == 1 || (force_bm == 2 && bm_auto(p)));
+  // window row pitch: a workgroup's 8 blocks span 16 (tc1 - tc0) + 32 <= 16 (S / 8 + 8) + 32
+  // bytes (<= 544 up to S = 192)
   g->bm_lp = S <= 64 ? 288 : 544;
   if (g->bm && (p.stride % 16 || (uintptr_t)p.cur % 16)) g->bm = 0;  // 16-byte cur row loads
   const int nxmax = min(48 + 2 * S + 1, W - 15);

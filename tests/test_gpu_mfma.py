@@ -35,7 +35,8 @@ def _check(engine, ref, cur, span, tag, stride=None):
     np.testing.assert_array_equal(cost, ocost, err_msg=tag)
 
 
-@pytest.mark.parametrize("span", [1, 2, 3, 7, 8, 13, 16, 17, 24, 31, 32, 40, 47, 48, 63, 64, 80, 103])
+@pytest.mark.parametrize("span", [1, 2, 3, 7, 8, 13, 16, 17, 24, 31, 32, 40, 47, 48, 63, 64, 80, 103,
+                                  104, 128, 150, 192])
 def test_mfma_ssd_spans(engine, span):
     """Every (64-column groups, chunk length) instance the planner picks, with
     frame edges on all sides and tiles that lack block rows or columns."""
@@ -197,3 +198,12 @@ def test_mfma_random_shapes(engine):
         tag = f"it{it} {h}x{w} B{blk} S{span}"
         np.testing.assert_array_equal(mv, omv, err_msg=tag)
         np.testing.assert_array_equal(cost, ocost, err_msg=tag)
+
+
+@pytest.mark.parametrize("span", [72, 128, 192])
+def test_mfma_bm_large_ranges_interior_pairs(engine, span):
+    """Block-major kernel beyond 16 tiles per band (segmented key index) on a
+    frame wide enough for interior block pairs (the mask-free fast path)."""
+    rng = np.random.default_rng(3000 + span)
+    ref, cur = _pair(rng, 144, 40 * 16 + 2 * span, dx=5, dy=-3)
+    _check(engine, ref, cur, span, f"S{span} wide")
