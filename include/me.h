@@ -90,11 +90,13 @@ const char* me_last_error(const me_ctx* ctx);
 const char* me_version(void);
 
 /* Kernel path (process-wide; A/B tests and diagnostics).  ME_PATH_AUTO: SSD
- * searches with 16x16 blocks run on the matrix cores (i8 MFMA), everything
- * else on the VALU kernels; ME_PATH_VALU: VALU kernels only.  Results are
- * identical either way.  The environment variable ME_PATH=valu sets the
- * initial value. */
-typedef enum { ME_PATH_AUTO = 0, ME_PATH_VALU = 1 } me_path;
+ * searches with 16x16 and 8x8 blocks run on the matrix cores (i8 MFMA),
+ * everything else on the VALU kernels; ME_PATH_VALU: VALU kernels only;
+ * ME_PATH_MFMA_TILES: as AUTO, but 16x16 SSD on the 4x4-block-tile MFMA kernel
+ * (the fallback for rows that are not 16-byte aligned) instead of the
+ * block-major one.  Results are identical on every path.  The environment
+ * variable ME_PATH=valu sets the initial value. */
+typedef enum { ME_PATH_AUTO = 0, ME_PATH_VALU = 1, ME_PATH_MFMA_TILES = 2 } me_path;
 void me_set_kernel_path(me_path path);
 
 /* Tiling helpers (src/common/prediction_frame.c:9-11). */

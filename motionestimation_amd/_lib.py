@@ -18,7 +18,7 @@ CSRC = os.path.join(PKG, "csrc")
 ME_OK, ME_EINVAL, ME_ENOMEM, ME_EDEVICE, ME_ECOMM, ME_EUNSUPPORTED, ME_EIO = range(7)
 ME_YUV_LUMA, ME_YUV_I420 = 0, 1
 ME_COST_SSD, ME_COST_SAD, ME_COST_SSIM = 0, 1, 2
-ME_PATH_AUTO, ME_PATH_VALU = 0, 1
+ME_PATH_AUTO, ME_PATH_VALU, ME_PATH_MFMA_TILES = 0, 1, 2
 ME_MAX_BLOCK, ME_MAX_RANGE = 64, 1024
 
 # Every symbol include/me.h declares, with (restype, argtypes).

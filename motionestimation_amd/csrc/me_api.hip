@@ -272,7 +272,9 @@ const char* me_last_error(const me_ctx* ctx) { return ctx ? ctx->err : "null con
 
 const char* me_version(void) { return "me_hip 1 gfx950"; }
 
-void me_set_kernel_path(me_path path) { me::set_force_valu(path == ME_PATH_VALU ? 1 : 0); }
+void me_set_kernel_path(me_path path) {
+  me::set_force_valu(path == ME_PATH_VALU ? 1 : path == ME_PATH_MFMA_TILES ? 2 : 0);
+}
 
 int me_num_blocks(int width, int height, int blk) {
   if (width <= 0 || height <= 0 || blk <= 0) return 0;

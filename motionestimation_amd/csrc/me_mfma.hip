@@ -1282,7 +1282,7 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_bm16_kernel(SearchArgs p, M
 }  // namespace
 
 // Process-wide path switch (me_set_kernel_path): A/B tests and diagnostics.
-static int g_force_valu = -1;
+static int g_force_valu = -1;  // 1: VALU kernels only; 2: no block-major kernel (me_set_kernel_path)
 void set_force_valu(int v) { g_force_valu = v; }
 bool mfma_disabled() {
   if (g_force_valu < 0) {
@@ -1329,7 +1329,7 @@ bool plan_mfma_ssd(const SearchArgs& p, MfmaGeom* g) {
     const char* e = getenv("ME_MFMA_BM");
     force_bm = e ? (e[0] == '1' ? 1 : e[0] == '0' ? 0 : 2) : 2;
   }
-  g->bm = S <= 192 && (force_bm == 1 || (force_bm == 2 && bm_auto(p)));
+  g->bm = S <= 192 && g_force_valu != 2 && (force_bm == 1 || (force_bm == 2 && bm_auto(p)));
   // window row pitch: a workgroup's 8 blocks span 16 (tc1 - tc0) + 32 <= 16 (S / 8 + 8) + 32
   // bytes (<= 544 up to S = 192)
   g->bm_lp = S <= 64 ? 288 : 544;

@@ -207,3 +207,18 @@ def test_mfma_bm_large_ranges_interior_pairs(engine, span):
     rng = np.random.default_rng(3000 + span)
     ref, cur = _pair(rng, 144, 40 * 16 + 2 * span, dx=5, dy=-3)
     _check(engine, ref, cur, span, f"S{span} wide")
+
+
+def test_mfma_tile_kernel_spans(engine):
+    """The 4x4-block-tile kernel (the fallback for rows that are not 16-byte
+    aligned), forced through me_set_kernel_path: every (column groups, chunk
+    length) instance against the oracle."""
+    rng = np.random.default_rng(77)
+    try:
+        me.set_kernel_path("tiles")
+        for span in (1, 7, 16, 17, 32, 47, 48, 64, 80, 103):
+            for (h, w) in [(96, 128), (150, 200)]:
+                ref, cur = _pair(rng, h, w, dx=(span % 5) - 2, dy=2 - (span % 3))
+                _check(engine, ref, cur, span, f"tiles {h}x{w} S{span}")
+    finally:
+        me.set_kernel_path("auto")
