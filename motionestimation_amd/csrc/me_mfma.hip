@@ -52,6 +52,9 @@
 #ifndef ME_MFMA_DLY
 #define ME_MFMA_DLY 1  // 1..3 (the 16-register accumulator ring holds 13 + DLY rows)
 #endif
+#ifndef ME_SSD8_KM
+#define ME_SSD8_KM 3  // 8x8 chunk length L = 16 KM: 48 rows (8K +-128: 64 rows 7.12 ms, 48 6.95-7.0, 32 8.3)
+#endif
 #ifndef ME_SSD8_WP
 #define ME_SSD8_WP 80  // 8x8 window copy pitch: 4 x 72 x 80 + S2 table = 40 KB, four workgroups per CU
 #endif
@@ -1436,7 +1439,7 @@ static bool plan_mfma_ssd8(const SearchArgs& p, MfmaGeom* g) {
   g->ngx = (nxmax + 63) / 64;
   g->ngxw = 1;
   if (g->ngx > 1 && (!p.mkeys || !p.mcnt || p.merge_tiles < mfma_merge_tiles(p))) return false;
-  g->km = 4;  // L = 64
+  g->km = ME_SSD8_KM;  // L = 16 km candidate rows per chunk
   const int L = 16 * g->km;
   g->lds = 4 * (L + 8) * ME_SSD8_WP + 16 * 8 + 16 * 4 + (L + 1) * 256;
   g->ya0 = max(r0 * 8 - S, 0);
@@ -1474,11 +1477,11 @@ hipError_t launch_mfma_ssd(const SearchArgs& p, const MfmaGeom& g, hipStream_t s
   if (p.blk == 8) {
     const dim3 grid8((unsigned)(g.tiles_x * g.tiles_y * g.ngx));
     if (g.lds > 64 * 1024) {
-      e = hipFuncSetAttribute((const void*)me_mfma_ssd8_kernel<4>,
+      e = hipFuncSetAttribute((const void*)me_mfma_ssd8_kernel<ME_SSD8_KM>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, g.lds);
       if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(me_mfma_ssd8_kernel<4>, grid8, dim3(256), g.lds, stream, p, g);
+    hipLaunchKernelGGL(me_mfma_ssd8_kernel<ME_SSD8_KM>, grid8, dim3(256), g.lds, stream, p, g);
     return hipGetLastError();
   }
   if (g.bm) {
