@@ -662,7 +662,7 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd16_kernel(SearchArgs p, 
 // same 32-bit key epilogue as the 16x16 kernel:
 //   key = ((S2 + 1) << 6) + (y - y0) + (acc << 7) = (SSD - p + 1) << 6 | (y - y0)
 // SSD <= 64 * 255^2 < 2^22, so valid keys < 2^28; x out of window: acc + 2^22
-// (keys in [2^29, 2^30)); y out of window: bit 31.  Chunks of L = 64 rows.
+// (keys in [2^29, 2^30)); y out of window: bit 31.  Chunks of L = 16 KM8 rows (48).
 // Workgroup = (tile, one group of 64 candidate columns), 4 waves (phase s);
 // tiles spanning several workgroups merge like the 16x16 kernel.
 template <int KM8>
@@ -1416,7 +1416,7 @@ bool plan_mfma_ssd(const SearchArgs& p, MfmaGeom* g) {
 }
 
 // 8x8 blocks: full-height block rows only (a partial bottom row goes to the
-// VALU kernels), one 64-column group per workgroup, chunks of 64 rows.
+// VALU kernels), one 64-column group per workgroup, chunks of 16 ME_SSD8_KM rows.
 static bool plan_mfma_ssd8(const SearchArgs& p, MfmaGeom* g) {
   if (mfma_disabled()) return false;
   const int S = p.range, W = p.width, H = p.height;
