@@ -6,15 +6,19 @@ GB/s vs roofline.  One step = one full search of a 1920x1080 Y-frame pair
 (B=16, S=32, SAD, 33,188,832 exact candidates) per rank, inputs resident in
 HBM before the timed region.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--mode frames|stripe]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--mode auto|frames|stripe]
                   [--config 1080p|4k|8k] [--cost sad|ssd] [--no-cpu]
 
---mode frames (default): each rank searches its own frame pair per step (a
-  sequence sharded across GPUs): weak scaling, no collective in the data path.
---mode stripe: ONE frame per step split into candidate-balanced block-row
-  stripes, one per rank, each rank holding only its stripe + S-row ref halo;
-  the per-stripe MV records are gathered to rank 0 with one RCCL gather inside
-  the timed step (strong scaling).
+--mode stripe (the default for N > 1, north_star's split): ONE frame per step
+  split into candidate-balanced block-row stripes, one per rank, each rank
+  holding only its stripe + S-row ref halo; the per-stripe MV records are
+  gathered to rank 0 with one RCCL gather per frame inside the timed region
+  (strong scaling).  Frames stream: the gather of frame k runs on
+  RCCL's stream while frame k+1 is searched (double-buffered records).
+--mode frames (the default for N = 1, where it is the same single search):
+  each rank searches its own frame pair per step: weak scaling, no collective.
+Every line also carries `stripe_4k`: BASELINE configs[3] (4K +-64) in stripe
+mode on the same ranks, with its gather parity.
 For N > 1 launch with torch.distributed.run (one process per GPU, RCCL).
 Rank 0 prints ONE JSON line.
 """
@@ -50,7 +54,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--mode", choices=["frames", "stripe"], default="frames")
+    ap.add_argument("--mode", choices=["auto", "frames", "stripe"], default="auto",
+                    help="auto: frames at N = 1, stripe at N > 1")
     ap.add_argument("--config", choices=list(CONFIGS), default="1080p")
     ap.add_argument("--cost", choices=["sad", "ssd", "ssim"], default="sad")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
@@ -58,7 +63,9 @@ def parse():
                     help="skip the SSD (matrix-core) line beside a SAD run")
     ap.add_argument("--no-stream", action="store_true",
                     help="skip the host frame-pair streaming leg (PCIe-inclusive, not `value`)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=16,
+                    help="threads of the main CPU-baseline leg (the GPU box's CPU share)")
+    ap.add_argument("--no-4k", action="store_true", help="skip the nested stripe_4k record")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="nccl = RCCL (production); gloo only to rehearse N ranks on one GPU")
     return ap.parse_args()
@@ -88,22 +95,41 @@ def cpu_baselines(ref, cur, blk, span, cost, threads, cands):
         what = f"block rows {r0}..{min(nby, r0 + 4) - 1} of the"
         cands = sum(_block_candidates(w, h, blk, span, i % nbx, i // nbx)
                     for i in range(begin, end))
-    times = []
-    for _ in range(5):
-        t0 = time.perf_counter()
-        O.full_search(ref, cur, blk, span, cost, threads=threads, begin=begin, end=end)
-        times.append(time.perf_counter() - t0)
-    med = statistics.median(times)
+    def port(nthreads, variant="", reps=5):
+        """median seconds of `reps` oracle searches over blocks [begin, end)"""
+        times = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            O.full_search(ref, cur, blk, span, cost, threads=nthreads, begin=begin, end=end,
+                          variant=variant)
+            times.append(time.perf_counter() - t0)
+        return statistics.median(times)
+
+    med = port(threads)
     cpu_model = ""
     try:
         with open("/proc/cpuinfo") as f:
             cpu_model = next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), "")
     except OSError:
         pass
+    affinity = len(os.sched_getaffinity(0))
     out = {"value": cands / med, "unit": "candidates/s", "cores": threads, "kind": "port",
-           "cpu_model": cpu_model, "host_cpus": os.cpu_count(),
+           "cpu_model": cpu_model, "host_cpus": os.cpu_count(), "affinity_cpus": affinity,
            "sample": f"{what} {w}x{h} B{blk} +-{span} {cost.upper()} frame, "
                      f"oracle/me_oracle.c -O2, {threads} pthreads, median of 5 ({med*1e3:.1f} ms)"}
+    # SURVEY §8d's other legs: the port with the reference's 100-thread pool
+    # (main.c:144) and with one thread per CPU of this process's affinity mask,
+    # and the port built without optimisation (as src/cpu/run.sh:4 builds).
+    legs = []
+    for n in sorted({100, affinity}):
+        m = port(n, reps=3)
+        legs.append({"threads": n, "value": cands / m, "unit": "candidates/s",
+                     "sample": f"same blocks, -O2, {n} pthreads, median of 3 ({m*1e3:.1f} ms)"})
+    out["port_threads"] = legs
+    m = port(threads, variant="O0", reps=3)
+    out["port_O0"] = {"threads": threads, "value": cands / m, "unit": "candidates/s",
+                      "sample": f"same blocks, oracle/liboracle_O0.so (-O0), {threads} pthreads, "
+                                f"median of 3 ({m*1e3:.1f} ms)"}
     # the reference binary at -O2, and as src/cpu/run.sh:4 builds it (-O0)
     for key, name, opt in (("reference_binary", "mes", "-O2"), ("reference_binary_O0", "mes_O0", "-O0")):
         mes = os.path.join(REPO, "oracle", "_ref", name)
@@ -180,6 +206,151 @@ def ssd_beside(eng, ref_t, cur_t, blk, span, nb, cands_frame, dev, steps):
                          "unit": "TFLOP/s", "frac": tops / I8_PEAK_TOPS}}
 
 
+class StripeRun:
+    """One frame per step in row stripes over the ranks.
+
+    Rank r holds its cur stripe and the ref rows with the S-row halo, searches
+    its block rows (me_full_search_stripe_device), and sends its padded
+    records to rank 0 in one gather per frame.  With RCCL the gather is
+    asynchronous on RCCL's stream and the records are double-buffered: the
+    gather of frame k overlaps the search of frame k + 1, and the search of
+    frame k + 2 waits (on the GPU) for the gather that read its buffer."""
+
+    def __init__(self, eng, dev, world, rank, gloo, ref, cur, blk, span, cost):
+        import torch
+        from motionestimation_amd import shard
+        h, w = ref.shape
+        self.eng, self.dev, self.world, self.rank, self.gloo = eng, dev, world, rank, gloo
+        self.w, self.h, self.blk, self.span, self.cost = w, h, blk, span, cost
+        self.stripes = shard.plan(w, h, blk, span, world)
+        self.st = st = self.stripes[rank]
+        self.ref_t = torch.from_numpy(ref[st.ref_y0:st.ref_y1].copy()).to(dev)
+        self.cur_t = torch.from_numpy(cur[st.cur_y0:st.cur_y1].copy()).to(dev)
+        self.recs = [torch.zeros((2, st.max_blocks), dtype=torch.int32, device=dev)
+                     for _ in range(2)]
+        cdev = torch.device("cpu") if gloo else dev
+        self.bufs = [[torch.empty_like(r, device=cdev) for _ in range(world)] if rank == 0
+                     else None for r in self.recs]
+        self.works = [None, None]
+        self.i = 0
+
+    def step(self):
+        import torch
+        import torch.distributed as dist
+        k = self.i & 1
+        self.i += 1
+        rec, st = self.recs[k], self.st
+        if self.works[k] is not None:  # the gather that read recs[k] (frame i - 2)
+            self.works[k].wait()       # RCCL: the current stream waits, not the host
+            self.works[k] = None
+        if st.nblocks:
+            mv = rec[0].view(torch.int16).view(st.max_blocks, 2)  # (mvx, mvy) int16 pairs
+            self.eng.search_stripe_device(self.ref_t, st.ref_y0, self.cur_t, st.cur_y0, self.w,
+                                          self.h, self.blk, self.span, self.cost, st.row_begin,
+                                          st.row_end, mv, rec[1])
+        if self.world > 1:  # the one exchange: per-stripe MV records -> rank 0
+            if self.gloo:
+                dist.gather(rec.cpu(), self.bufs[k], dst=0)
+            else:
+                self.works[k] = dist.gather(rec, self.bufs[k], dst=0, async_op=True)
+        return k
+
+    def drain(self):
+        for k in range(2):
+            if self.works[k] is not None:
+                self.works[k].wait()
+                self.works[k] = None
+
+    def gathered_field(self):
+        """A last, synchronous frame; rank 0 returns the assembled (mv, cost)."""
+        import torch
+        from motionestimation_amd import shard
+        k = self.step()
+        self.drain()
+        torch.cuda.synchronize()
+        if self.rank != 0:
+            return None
+        if self.world == 1:
+            rec = self.recs[k].cpu()
+            return shard.assemble([rec], self.stripes)
+        return shard.assemble(self.bufs[k], self.stripes)
+
+
+def timed(step, steps, warmup, world, finish=None):
+    """W untimed steps, then K steps between barrier + synchronize; returns
+    (max-over-ranks wall seconds, max-over-ranks ms per step on the current
+    stream from one HIP event pair around the region)."""
+    import torch
+    import torch.distributed as dist
+    for _ in range(warmup):
+        step()
+    if finish:
+        finish()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev0.record()
+    for _ in range(steps):
+        step()
+    if finish:
+        finish()
+    ev1.record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = ev0.elapsed_time(ev1) / steps
+    if world > 1:
+        gloo = dist.get_backend() == "gloo"
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64,
+                         device="cpu" if gloo else torch.device("cuda", torch.cuda.current_device()))
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+    return elapsed, kern_ms
+
+
+def stripe_parity(eng, sr, ref, cur, dev):
+    """Rank 0: the gathered stripe field equals one full-frame search (not timed)."""
+    import torch
+    field = sr.gathered_field()
+    if sr.rank != 0:
+        return None
+    gmv, gcost = field
+    h, w = ref.shape
+    import motionestimation_amd as me
+    nb = me.num_blocks(w, h, sr.blk)
+    fmv = torch.empty((nb, 2), dtype=torch.int16, device=dev)
+    fco = torch.empty(nb, dtype=torch.int32, device=dev)
+    eng.full_search_device(torch.from_numpy(ref).to(dev), torch.from_numpy(cur).to(dev), sr.blk,
+                           sr.span, sr.cost, fmv, fco)
+    torch.cuda.synchronize()
+    return bool(np.array_equal(gmv, fmv.cpu().numpy()) and
+                np.array_equal(gcost, fco.cpu().numpy().view(np.uint32)))
+
+
+def stripe_record(eng, dev, world, rank, gloo, cfg_name, cost, steps, warmup):
+    """Nested record: a BASELINE config in stripe mode on the same ranks."""
+    import motionestimation_amd as me
+    from motionestimation_amd import synth
+    cfg, blk, span = CONFIGS[cfg_name]
+    w, h, seed, sx, sy = synth.CONFIGS[cfg]
+    ref, cur = synth.frame_pair(w, h, seed, sx, sy)
+    cands = me.candidate_count(w, h, blk, span)
+    sr = StripeRun(eng, dev, world, rank, gloo, ref, cur, blk, span, cost)
+    elapsed, kern_ms = timed(sr.step, steps, warmup, world, sr.drain)
+    parity = stripe_parity(eng, sr, ref, cur, dev)
+    return {"value": cands * steps / elapsed, "unit": "candidates/s",
+            "frames_per_s": steps / elapsed, "ms_per_step": elapsed / steps * 1e3,
+            "kernel_ms": kern_ms, "steps": steps, "warmup": warmup, "n_gpus": world,
+            "scaling": "strong", "parallelism": f"stripe{world}",
+            "workload": f"{w}x{h} Y, {blk}x{blk} blocks, full search +-{span}, {cost.upper()}, "
+                        "one frame per step in row stripes + one RCCL gather per frame",
+            "candidates_per_frame": cands, "stripe_gather_parity": parity}
+
+
 def load_traffic(tag):
     """HBM bytes per launch from the committed rocprofv3 PMC summary of this
     workload (tools/profile.sh), or None."""
@@ -214,7 +385,7 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
 
     import motionestimation_amd as me
-    from motionestimation_amd import shard, synth
+    from motionestimation_amd import synth
 
     cfg, blk, span = CONFIGS[args.config]
     w, h, seed, sx, sy = synth.CONFIGS[cfg]
@@ -222,7 +393,9 @@ def main():
     nb = me.num_blocks(w, h, blk)
     eng = me.Engine(devices=[gpu])
 
-    if args.mode == "frames":
+    mode = args.mode if args.mode != "auto" else ("frames" if world == 1 else "stripe")
+    parity = None
+    if mode == "frames":
         # rank r: its own frame pair of the sequence (same size; seed varies)
         ref, cur = synth.frame_pair(w, h, seed + rank, sx, sy)
         ref_t = torch.from_numpy(ref).to(dev)
@@ -233,72 +406,23 @@ def main():
         def step():
             eng.full_search_device(ref_t, cur_t, blk, span, args.cost, mv_t, cost_t)
         units_per_step = cands_frame * world
+        # Kernel duration: one HIP event pair on the stream the search is
+        # launched on (torch's current stream) around the whole timed region,
+        # / K (per-step event pairs would stretch the back-to-back launches).
+        elapsed, kern_ms = timed(step, args.steps, args.warmup, world)
     else:
         ref, cur = synth.frame_pair(w, h, seed, sx, sy)
-        stripes = shard.plan(w, h, blk, span, world)
-        st = stripes[rank]
-        ref_t = torch.from_numpy(ref[st.ref_y0:st.ref_y1].copy()).to(dev)
-        cur_t = torch.from_numpy(cur[st.cur_y0:st.cur_y1].copy()).to(dev)
-        rec = torch.zeros((2, st.max_blocks), dtype=torch.int32, device=dev)
-        mv_view = rec[0].view(torch.int16).view(st.max_blocks, 2)
-        cost_view = rec[1]
-        cdev = torch.device("cpu") if gloo else dev
-        bufs = [torch.empty_like(rec, device=cdev) for _ in range(world)] if rank == 0 else None
-
-        def step():
-            if st.nblocks:
-                eng.search_stripe_device(ref_t, st.ref_y0, cur_t, st.cur_y0, w, h, blk, span,
-                                         args.cost, st.row_begin, st.row_end, mv_view, cost_view)
-            if world > 1:  # the one exchange: per-stripe MV records -> rank 0 (RCCL)
-                dist.gather(rec.cpu() if gloo else rec, bufs, dst=0)
+        sr = StripeRun(eng, dev, world, rank, gloo, ref, cur, blk, span, args.cost)
+        st = sr.st
         units_per_step = cands_frame
-
-    # warmup (untimed)
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-
-    # Kernel duration: one HIP event pair on the stream the search is launched
-    # on (torch's current stream) around the whole timed region, / K.  Per-step
-    # event pairs would insert a marker between every two launches and stretch
-    # the measured step; the region average is the back-to-back launch time.
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ev0.record()
-    for _ in range(args.steps):
-        step()
-    ev1.record()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    kern_ms = ev0.elapsed_time(ev1) / args.steps
-    if world > 1:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64,
-                         device="cpu" if gloo else dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms = float(t[0]), float(t[1])
-
-    parity = None
-    if args.mode == "stripe" and rank == 0 and world > 1:
-        # the gathered field equals a single-GPU full-frame search (not timed)
-        gmv, gcost = shard.assemble(bufs, stripes)
-        fmv = torch.empty((nb, 2), dtype=torch.int16, device=dev)
-        fco = torch.empty(nb, dtype=torch.int32, device=dev)
-        eng.full_search_device(torch.from_numpy(ref).to(dev), torch.from_numpy(cur).to(dev), blk,
-                               span, args.cost, fmv, fco)
-        torch.cuda.synchronize()
-        parity = bool(np.array_equal(gmv, fmv.cpu().numpy()) and
-                      np.array_equal(gcost, fco.cpu().numpy().view(np.uint32)))
+        elapsed, kern_ms = timed(sr.step, args.steps, args.warmup, world, sr.drain)
+        parity = stripe_parity(eng, sr, ref, cur, dev)
 
     value = units_per_step * args.steps / elapsed
     # Roofline of the dominant kernel: algorithmic HBM bytes per
     # launch = 2*W*H (u8 ref + cur, read once) + 8*nblocks (mv + cost written)
     # for the planes that launch covers.
-    if args.mode == "frames":
+    if mode == "frames":
         alg_bytes = 2 * w * h + 8 * nb
         absdiffs = cands_frame * blk * blk
     else:
@@ -317,17 +441,17 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak" if args.mode == "frames" else "strong",
+        "scaling": "weak" if mode == "frames" else "strong",
         "vs_baseline": None,
         "dtype": "u8",
         "data": f"synthetic: motionestimation_amd.synth '{cfg}' (splitmix64 seed {seed}"
-                f"{'+rank' if args.mode == 'frames' else ''}, 5x5 box, cur = ref shifted "
+                f"{'+rank' if mode == 'frames' and world > 1 else ''}, 5x5 box, cur = ref shifted "
                 f"({sx:+d},{sy:+d}) + uniform [-2,2])",
         "config": {"workload": f"{w}x{h} Y, {blk}x{blk} blocks, full search +-{span}, "
-                               f"{args.cost.upper()}, {'one frame pair per rank per step' if args.mode == 'frames' else 'one frame per step in row stripes + RCCL gather'}",
+                               f"{args.cost.upper()}, {'one frame pair per rank per step' if mode == 'frames' else 'one frame per step in row stripes + one RCCL gather per frame'}",
                    "width": w, "height": h, "block": blk, "range": span, "cost": args.cost,
                    "candidates_per_frame": cands_frame, "blocks_per_frame": nb,
-                   "parallelism": f"{args.mode}{world}"},
+                   "parallelism": f"{mode}{world}"},
         "kernel_ms": kern_ms,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
@@ -342,7 +466,7 @@ def main():
     if args.cost == "ssd" and blk in (8, 16):
         # B = 8 and 16 SSD run on the matrix cores (i8 MFMA cross term): the bound is
         # the MFMA peak; algorithmic ops = 2 x B*B multiply-adds per candidate
-        ops = 2.0 * blk * blk * (cands_frame if args.mode == "frames" else cands_frame / world)
+        ops = 2.0 * blk * blk * (cands_frame if mode == "frames" else cands_frame / world)
         tops = ops / (kern_ms / 1e3) / 1e12
         hbm = line["roofline"]
         hbm.pop("valu", None)
@@ -352,7 +476,7 @@ def main():
                                     "(S2 prepass + MFMA kernel); dense i8 peak",
                             "hbm": {k: hbm[k] for k in ("achieved", "peak", "unit", "frac",
                                                         "algorithmic_bytes_per_launch")}}
-    if (rank == 0 and world == 1 and args.mode == "frames" and args.cost == "sad"
+    if (rank == 0 and world == 1 and mode == "frames" and args.cost == "sad"
             and blk == 16 and not args.no_ssd):
         line["ssd_mfma"] = ssd_beside(eng, ref_t, cur_t, blk, span, nb, cands_frame, dev,
                                       min(args.steps, 20))
@@ -361,7 +485,14 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baselines(ref, cur, blk, span, args.cost, args.cpu_threads,
                                              cands_frame)
-    if rank == 0 and world == 1 and args.mode == "frames" and not args.no_stream:
+    if not args.no_4k and args.cost in ("sad", "ssd"):
+        # BASELINE configs[3] (4K +-64), the config north_star's 8-GPU split is
+        # quoted on, in stripe mode on the same ranks (at N = 1: the denominator)
+        rec4k = stripe_record(eng, dev, world, rank, gloo, "4k", args.cost,
+                              min(args.steps, 20), min(args.warmup, 3))
+        if rank == 0:
+            line["stripe_4k"] = rec4k
+    if rank == 0 and world == 1 and mode == "frames" and not args.no_stream:
         line["host_stream"] = host_stream(eng, w, h, blk, span, args.cost, seed, sx, sy,
                                           kern_ms, cands_frame)
     if rank == 0:

@@ -95,7 +95,8 @@ const char* me_version(void);
  * ME_PATH_MFMA_TILES: as AUTO, but 16x16 SSD on the 4x4-block-tile MFMA kernel
  * (the fallback for rows that are not 16-byte aligned) instead of the
  * block-major one.  Results are identical on every path.  The environment
- * variable ME_PATH=valu sets the initial value. */
+ * variable ME_PATH=auto|valu|tiles sets the initial value (anything else is
+ * ignored with a message on stderr). */
 typedef enum { ME_PATH_AUTO = 0, ME_PATH_VALU = 1, ME_PATH_MFMA_TILES = 2 } me_path;
 void me_set_kernel_path(me_path path);
 

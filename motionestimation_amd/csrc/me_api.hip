@@ -12,7 +12,9 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "me_internal.h"
@@ -20,6 +22,73 @@
 using me::Dev;
 
 namespace me {
+
+// ------------------------------------------------------------ tuning knobs
+#ifdef ME_TUNING
+// Diagnostic build only (libme_hip_tune.so): validated environment overrides.
+static bool env_int(const char* name, int lo, int hi, int* out) {
+  const char* e = getenv(name);
+  if (!e || !*e) return false;
+  char* end = nullptr;
+  const long v = strtol(e, &end, 10);
+  if (*end || v < lo || v > hi) {
+    fprintf(stderr, "me_hip: ignoring %s=%s (expected an integer in [%d, %d])\n", name, e, lo, hi);
+    return false;
+  }
+  *out = (int)v;
+  return true;
+}
+
+static Tuning read_tuning() {
+  Tuning t;
+  if (const char* e = getenv("ME_PLAN")) {
+    int v[5] = {0, 0, 0, 0, -1};
+    const int n = sscanf(e, "%d,%d,%d,%d,%d", &v[0], &v[1], &v[2], &v[3], &v[4]);
+    const bool ok = n >= 4 && (v[0] == 0 || v[0] == 8 || v[0] == 11 || v[0] == 13) &&
+                    v[1] >= 0 && v[1] <= 16 && v[2] >= 0 && v[2] <= 64 &&
+                    (v[3] == 0 || (v[3] >= 64 && v[3] <= 1024 && v[3] % 64 == 0)) &&
+                    v[4] >= -1 && v[4] <= 1;
+    if (ok) {
+      t.plan_k = v[0]; t.plan_tb = v[1]; t.plan_cpp = v[2]; t.plan_threads = v[3]; t.plan_fold = v[4];
+    } else {
+      fprintf(stderr, "me_hip: ignoring ME_PLAN=%s (K in {0,8,11,13}, tb 0..16, cpp 0..64, "
+                      "threads 0 or 64..1024 step 64, fold -1..1)\n", e);
+    }
+  }
+  env_int("ME_DYN", 0, 1 << 20, &t.dyn);
+  env_int("ME_MFMA_BM", 0, 1, &t.mfma_bm);
+  env_int("ME_MFMA_KM", 2, 3, &t.mfma_km);
+  env_int("ME_MFMA_NGXW", 1, 2, &t.mfma_ngxw);
+  env_int("ME_STREAM_COOL", 1, 64, &t.stream_cool);
+  env_int("ME_STREAM_AHEAD", 1, 9, &t.stream_ahead);
+  return t;
+}
+const Tuning& tuning() {
+  static const Tuning t = read_tuning();  // once, thread-safe (C++11 static init)
+  return t;
+}
+#else
+const Tuning& tuning() {
+  static const Tuning t;  // automatic settings; the product reads no tuning knobs
+  return t;
+}
+#endif
+
+// ME_PATH (include/me.h): initial kernel path; me_set_kernel_path overrides it.
+static int initial_path() {
+  const char* e = getenv("ME_PATH");
+  if (!e || !*e || !strcmp(e, "auto")) return 0;
+  if (!strcmp(e, "valu")) return 1;
+  if (!strcmp(e, "tiles")) return 2;
+  fprintf(stderr, "me_hip: ignoring ME_PATH=%s (auto | valu | tiles)\n", e);
+  return 0;
+}
+static std::atomic<int>& path_code() {
+  static std::atomic<int> v{initial_path()};
+  return v;
+}
+int kernel_path() { return path_code().load(std::memory_order_relaxed); }
+void set_kernel_path_code(int v) { path_code().store(v, std::memory_order_relaxed); }
 
 me_status fail(me_ctx* c, me_status s, const char* fmt, ...) {
   if (c) {
@@ -127,6 +196,21 @@ me_status attach_scratch(me_ctx* c, Dev& d, SearchArgs& p) {
   return ME_OK;
 }
 
+me_status launch_ordered(me_ctx* c, Dev& d, SearchArgs& p, hipStream_t s) {
+  if (d.searched && d.search_stream != s) HIPCHK(c, hipStreamWaitEvent(s, d.search_ev, 0));
+  const hipError_t e = launch_search(p, s, nullptr);
+  if (e != hipSuccess) {
+    (void)hipMemsetAsync(d.sched, 0, 64, s);
+    if (d.mkeys) (void)hipMemsetAsync(d.mkeys, 0xFF, d.merge_cap * 16 * 8, s);
+    if (d.mcnt) (void)hipMemsetAsync(d.mcnt, 0, d.merge_cap * 4, s);
+    return fail(c, ME_EDEVICE, "search launch: %s", hipGetErrorString(e));
+  }
+  HIPCHK(c, hipEventRecord(d.search_ev, s));
+  d.search_stream = s;
+  d.searched = true;
+  return ME_OK;
+}
+
 }  // namespace me
 
 namespace {
@@ -136,6 +220,7 @@ using me::grow;
 using me::check_args;
 using me::make_args;
 using me::attach_scratch;
+using me::launch_ordered;
 
 uint64_t row_candidates(int width, int height, int blk, int range, int by) {
   const int nbx = (width + blk - 1) / blk;
@@ -170,13 +255,46 @@ me_status ensure_comms(me_ctx* c) {
   return ME_OK;
 }
 
-// Multi-device frame search: row stripes, one per context device, then one
-// gather of the padded per-stripe record arrays to device 0.
+// One stripe of a multi-device search on its device: upload the cur stripe
+// and the ref rows with the S-row halo, then launch (the calling thread owns d).
+me_status stripe_upload_launch(me_ctx* c, Dev& d, const uint8_t* ref, const uint8_t* cur,
+                               int width, int height, int stride, int blk, int range, int cost,
+                               int r0, int r1, size_t max_blocks) {
+  HIPCHK(c, hipSetDevice(d.id));
+  const int y_ref0 = r0 * blk - range > 0 ? r0 * blk - range : 0;
+  const int y_ref1 = r1 * blk + range < height ? r1 * blk + range : height;
+  const int y_cur0 = r0 * blk;
+  const int y_cur1 = r1 * blk < height ? r1 * blk : height;
+  const size_t ref_rows = r1 > r0 ? (size_t)(y_ref1 - y_ref0) : 0;
+  const size_t cur_rows = r1 > r0 ? (size_t)(y_cur1 - y_cur0) : 0;
+  me_status s;
+  if ((s = grow(c, (void**)&d.ref, &d.frame_cap, (ref_rows + cur_rows + 1) * width)) != ME_OK)
+    return s;
+  d.cur = d.ref + ref_rows * width;
+  if ((s = grow(c, (void**)&d.rec, &d.rec_cap, max_blocks * 8)) != ME_OK) return s;
+  if (r1 <= r0) return ME_OK;
+  HIPCHK(c, hipMemcpy2DAsync(d.ref, width, ref + (size_t)y_ref0 * stride, stride, width,
+                             ref_rows, hipMemcpyHostToDevice, d.stream));
+  HIPCHK(c, hipMemcpy2DAsync(d.cur, width, cur + (size_t)y_cur0 * stride, stride, width,
+                             cur_rows, hipMemcpyHostToDevice, d.stream));
+  int16_t* dmv = reinterpret_cast<int16_t*>(d.rec);
+  uint32_t* dcost = reinterpret_cast<uint32_t*>(d.rec + max_blocks * 4);
+  me::SearchArgs p = make_args(d.ref, y_ref0, d.cur, y_cur0, width, height, width, blk, range,
+                               cost, r0, r1, dmv, dcost);
+  if ((s = attach_scratch(c, d, p)) != ME_OK) return s;
+  return launch_ordered(c, d, p, d.stream);
+}
+
+// Multi-device frame search: row stripes balanced by candidate count, one per
+// context device.  One host thread per device uploads its stripe
+// (pageable host planes are staged by the runtime, so the uploads of the
+// devices overlap instead of running one after another) and enqueues its
+// search; then one ncclGather of the padded per-stripe records to device 0.
 me_status multi_search(me_ctx* c, const uint8_t* ref, const uint8_t* cur, int width,
                        int height, int stride, int blk, int range, int cost, int16_t* mv_xy,
                        uint32_t* block_cost) {
   const int n = (int)c->devs.size();
-  const int nby = (height + blk - 1) / blk, nbx = (width + blk - 1) / blk;
+  const int nbx = (width + blk - 1) / blk;
   std::vector<int> bounds(n + 1);
   me_status s = me_plan_stripes(width, height, blk, range, n, bounds.data());
   if (s != ME_OK) return fail(c, s, "stripe plan");
@@ -186,31 +304,19 @@ me_status multi_search(me_ctx* c, const uint8_t* ref, const uint8_t* cur, int wi
   const size_t max_blocks = (size_t)(max_rows > 0 ? max_rows : 1) * nbx;
   const size_t rec_bytes = max_blocks * 8;
 
-  for (int i = 0; i < n; i++) {
-    Dev& d = c->devs[i];
-    HIPCHK(c, hipSetDevice(d.id));
-    const int r0 = bounds[i], r1 = bounds[i + 1];
-    const int y_ref0 = r0 * blk - range > 0 ? r0 * blk - range : 0;
-    const int y_ref1 = r1 * blk + range < height ? r1 * blk + range : height;
-    const int y_cur0 = r0 * blk;
-    const int y_cur1 = r1 * blk < height ? r1 * blk : height;
-    const size_t ref_rows = r1 > r0 ? (size_t)(y_ref1 - y_ref0) : 0;
-    const size_t cur_rows = r1 > r0 ? (size_t)(y_cur1 - y_cur0) : 0;
-    if ((s = grow(c, (void**)&d.ref, &d.frame_cap, (ref_rows + cur_rows + 1) * width)) != ME_OK)
-      return s;
-    d.cur = d.ref + ref_rows * width;
-    if ((s = grow(c, (void**)&d.rec, &d.rec_cap, rec_bytes)) != ME_OK) return s;
-    if (r1 <= r0) continue;
-    HIPCHK(c, hipMemcpy2DAsync(d.ref, width, ref + (size_t)y_ref0 * stride, stride, width,
-                               ref_rows, hipMemcpyHostToDevice, d.stream));
-    HIPCHK(c, hipMemcpy2DAsync(d.cur, width, cur + (size_t)y_cur0 * stride, stride, width,
-                               cur_rows, hipMemcpyHostToDevice, d.stream));
-    int16_t* dmv = reinterpret_cast<int16_t*>(d.rec);
-    uint32_t* dcost = reinterpret_cast<uint32_t*>(d.rec + max_blocks * 4);
-    me::SearchArgs p = make_args(d.ref, y_ref0, d.cur, y_cur0, width, height, width, blk, range,
-                                 cost, r0, r1, dmv, dcost);
-    if ((s = attach_scratch(c, d, p)) != ME_OK) return s;
-    HIPCHK(c, me::launch_search(p, d.stream, nullptr));
+  {
+    std::vector<me_ctx> errs(n);
+    std::vector<me_status> st(n, ME_OK);
+    std::vector<std::thread> th;
+    th.reserve(n);
+    for (int i = 0; i < n; i++)
+      th.emplace_back([&, i]() {
+        st[i] = stripe_upload_launch(&errs[i], c->devs[i], ref, cur, width, height, stride, blk,
+                                     range, cost, bounds[i], bounds[i + 1], max_blocks);
+      });
+    for (auto& t : th) t.join();
+    for (int i = 0; i < n; i++)
+      if (st[i] != ME_OK) return fail(c, st[i], "device %d: %s", c->devs[i].id, errs[i].err);
   }
   Dev& root = c->devs[0];
   HIPCHK(c, hipSetDevice(root.id));
@@ -247,7 +353,6 @@ me_status multi_search(me_ctx* c, const uint8_t* ref, const uint8_t* cur, int wi
     memcpy(mv_xy + 2 * off, base, (size_t)nblk * 4);
     if (block_cost) memcpy(block_cost + off, base + max_blocks * 4, (size_t)nblk * 4);
   }
-  (void)nby;
   return ME_OK;
 }
 
@@ -273,7 +378,7 @@ const char* me_last_error(const me_ctx* ctx) { return ctx ? ctx->err : "null con
 const char* me_version(void) { return "me_hip 1 gfx950"; }
 
 void me_set_kernel_path(me_path path) {
-  me::set_force_valu(path == ME_PATH_VALU ? 1 : path == ME_PATH_MFMA_TILES ? 2 : 0);
+  me::set_kernel_path_code(path == ME_PATH_VALU ? 1 : path == ME_PATH_MFMA_TILES ? 2 : 0);
 }
 
 int me_num_blocks(int width, int height, int blk) {
@@ -342,7 +447,8 @@ me_status me_create(me_ctx** out, const int* device_ids, int n) {
     d.id = id;
     if (hipSetDevice(id) != hipSuccess ||
         hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc((void**)&d.sched, 64) != hipSuccess || hipMemset(d.sched, 0, 64) != hipSuccess) {
+        hipMalloc((void**)&d.sched, 64) != hipSuccess || hipMemset(d.sched, 0, 64) != hipSuccess ||
+        hipEventCreateWithFlags(&d.search_ev, hipEventDisableTiming) != hipSuccess) {
       c->devs.push_back(d);
       me_destroy(c);
       (void)hipSetDevice(prev);
@@ -374,6 +480,7 @@ void me_destroy(me_ctx* c) {
     (void)hipFree(d.mkeys);
     (void)hipFree(d.mcnt);
     me::release_pipeline(d);
+    if (d.search_ev) (void)hipEventDestroy(d.search_ev);
     if (d.stream) (void)hipStreamDestroy(d.stream);
   }
   delete c;
@@ -402,7 +509,7 @@ me_status me_full_search(me_ctx* c, const uint8_t* ref, const uint8_t* cur, int 
   me::SearchArgs p = make_args(d.ref, 0, d.cur, 0, width, height, width, blk, range, cost, 0,
                                nby, dmv, dcost);
   if ((s = attach_scratch(c, d, p)) != ME_OK) return s;
-  HIPCHK(c, me::launch_search(p, d.stream, nullptr));
+  if ((s = launch_ordered(c, d, p, d.stream)) != ME_OK) return s;
   HIPCHK(c, hipMemcpyAsync(mv_xy, dmv, nb * 4, hipMemcpyDeviceToHost, d.stream));
   if (block_cost)
     HIPCHK(c, hipMemcpyAsync(block_cost, dcost, nb * 4, hipMemcpyDeviceToHost, d.stream));
@@ -426,8 +533,7 @@ me_status me_full_search_stripe_device(me_ctx* c, const uint8_t* d_ref, int ref_
   me::SearchArgs p = make_args(d_ref, ref_row0, d_cur, cur_row0, width, height, stride, blk,
                                range, cost, r0, r1, d_mv, d_cost);
   if ((s = attach_scratch(c, c->devs[0], p)) != ME_OK) return s;
-  HIPCHK(c, me::launch_search(p, (hipStream_t)stream, nullptr));
-  return ME_OK;
+  return launch_ordered(c, c->devs[0], p, (hipStream_t)stream);
 }
 
 me_status me_full_search_device(me_ctx* c, const uint8_t* d_ref, const uint8_t* d_cur,

@@ -11,6 +11,7 @@
 
 #include "me.h"
 #include "me_kernels.h"
+#include "me_tuning.h"
 
 namespace me {
 
@@ -34,6 +35,12 @@ struct Dev {
   unsigned long long* mkeys = nullptr;  // MFMA SSD merge keys (~0) and tile counters (0):
   uint32_t* mcnt = nullptr;             //   initialised on allocation, self-resetting after
   size_t merge_cap = 0;                 //   (tiles)
+  // The counters, merge keys and scratch above serve one search at a time:
+  // search_ev marks the end of the last search (on search_stream); a search
+  // issued on another stream waits for it first (launch_ordered).
+  hipEvent_t search_ev = nullptr;
+  hipStream_t search_stream = nullptr;
+  bool searched = false;
   // Frame-pair pipeline (me_stream.hip), kept across calls.
   std::vector<uint8_t*> slots;        // device frames, slot_bytes each
   std::vector<hipEvent_t> slot_ready; // upload of the slot's frame done (copy stream)
@@ -59,9 +66,16 @@ SearchArgs make_args(const uint8_t* ref, int ref_row0, const uint8_t* cur, int c
                      int r1, int16_t* mv, uint32_t* cst);
 
 // Point p at d's search scratch, growing it to what p's search needs.  A
-// device's scratch serves one search at a time: searches of one context are
-// stream-ordered (one stream per device, or the caller's stream).
+// device's scratch serves one search at a time: launch searches that use it
+// with launch_ordered.
 me_status attach_scratch(me_ctx* c, Dev& d, SearchArgs& p);
+
+// Launch p (scratch attached) on stream s after every earlier search of d:
+// a search arriving on a different stream than the previous one first waits
+// for that search's end event.  A failed launch re-zeroes the self-resetting
+// tile counters and merge buffers (a partly run kernel may have left them
+// dirty) before returning ME_EDEVICE.
+me_status launch_ordered(me_ctx* c, Dev& d, SearchArgs& p, hipStream_t s);
 
 // Pinned host ranges handed out by me_host_alloc (the pair pipeline DMAs
 // straight from them instead of staging).

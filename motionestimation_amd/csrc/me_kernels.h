@@ -89,7 +89,6 @@ bool plan_mfma_ssd(const SearchArgs& p, MfmaGeom* g);
 hipError_t launch_mfma_ssd(const SearchArgs& p, const MfmaGeom& g, hipStream_t stream);
 size_t mfma_ssd_scratch(const SearchArgs& p);  // 0: path not applicable
 bool mfma_disabled();
-void set_force_valu(int v);  // 1: VALU kernels only, 0: automatic
 
 hipError_t launch_search(const SearchArgs& p, hipStream_t stream, int* used_fast);
 hipError_t launch_generic(const SearchArgs& p, int bx0, int nbx_range, int row0, int nrows,

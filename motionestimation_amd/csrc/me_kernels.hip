@@ -28,6 +28,7 @@
 #include <type_traits>
 
 #include "me_kernels.h"
+#include "me_tuning.h"
 
 #ifndef ME_ABLATE
 #define ME_ABLATE 0  // diagnostic builds only (csrc/Makefile ablate); never shipped
@@ -829,14 +830,10 @@ bool plan_fast(const SearchArgs& p, QsadGeom* g, int* k_out) {
   // for one ds_read of B bytes (b*B + 2S multiple of B: S % 8 == 0 for B = 16).
   const bool fold_ok = sad && S % 4 == 0 && (B == 8 || S % 8 == 0);
   static const int Ks[] = {13, 11, 8};
-  // Tuning override (tools/plan_sweep.py only): ME_PLAN="K,tb,cpp,threads[,fold]",
-  // 0 = free (fold: -1 = free); read once per process.
-  static int force[5] = {-1, 0, 0, 0, -1};
-  if (force[0] < 0) {
-    force[0] = 0;
-    if (const char* e = getenv("ME_PLAN"))
-      sscanf(e, "%d,%d,%d,%d,%d", &force[0], &force[1], &force[2], &force[3], &force[4]);
-  }
+  // Tuning build override (tools/plan_sweep.py): ME_PLAN="K,tb,cpp,threads[,fold]",
+  // validated in me_api.hip; 0 = free (fold: -1 = free).
+  const Tuning& tu = tuning();
+  const int force[5] = {tu.plan_k, tu.plan_tb, tu.plan_cpp, tu.plan_threads, tu.plan_fold};
   const int thr = force[3] > 0 ? force[3] : 256;
   const int rows = p.block_row_end - p.block_row_begin;
   double best = -1;
@@ -911,13 +908,9 @@ bool plan_fast(const SearchArgs& p, QsadGeom* g, int* k_out) {
   g->fold = bF;
   g->groups = bG;
   // Dynamic tile pulls from this many tiles per workgroup on (ME_DYN overrides
-  // for tuning; 0 = static bands only).
+  // in the tuning build; 0 = static bands only).
   {
-    static int dyn_env = -2;
-    if (dyn_env == -2) {
-      const char* e = getenv("ME_DYN");
-      dyn_env = e ? atoi(e) : -1;
-    }
+    const int dyn_env = tu.dyn;
     // 3: measured (tools/dyn_sweep.sh) -- 4K (3.96 tiles/WG) and 8K gain
     // (8K -11 % with stealing), 1080p (2.7 tiles/WG) loses: its workgroups
     // start items in lockstep and the item-start pulls serialise on the

@@ -48,6 +48,7 @@
 #include <type_traits>
 
 #include "me_kernels.h"
+#include "me_tuning.h"
 
 #ifndef ME_MFMA_DLY
 #define ME_MFMA_DLY 1  // 1..3 (the 16-register accumulator ring holds 13 + DLY rows)
@@ -1284,16 +1285,8 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_bm16_kernel(SearchArgs p, M
 
 }  // namespace
 
-// Process-wide path switch (me_set_kernel_path): A/B tests and diagnostics.
-static int g_force_valu = -1;  // 1: VALU kernels only; 2: no block-major kernel (me_set_kernel_path)
-void set_force_valu(int v) { g_force_valu = v; }
-bool mfma_disabled() {
-  if (g_force_valu < 0) {
-    const char* e = getenv("ME_PATH");
-    g_force_valu = (e && e[0] == 'v') ? 1 : 0;  // ME_PATH=valu
-  }
-  return g_force_valu == 1;
-}
+// Process-wide path switch (me_set_kernel_path / ME_PATH, me_tuning.h).
+bool mfma_disabled() { return kernel_path() == 1; }
 
 // Tiles of a B = 16 search over block rows [begin, end) (the merge buffers' size).
 size_t mfma_merge_tiles(const SearchArgs& p) {
@@ -1326,13 +1319,9 @@ bool plan_mfma_ssd(const SearchArgs& p, MfmaGeom* g) {
   const int S = p.range, W = p.width, H = p.height;
   if (S < 1 || W < 16 || H < 16) return false;
   if (p.stride % 4 || (uintptr_t)p.cur % 4 || (uintptr_t)p.ref % 4) return false;
-  // block-major kernel for S <= 192 (ME_MFMA_BM=0|1: tuning override, read once)
-  static int force_bm = -1;
-  if (force_bm < 0) {
-    const char* e = getenv("ME_MFMA_BM");
-    force_bm = e ? (e[0] == '1' ? 1 : e[0] == '0' ? 0 : 2) : 2;
-  }
-  g->bm = S <= 192 && g_force_valu != 2 && (force_bm == 1 || (force_bm == 2 && bm_auto(p)));
+  // block-major kernel for S <= 192 (ME_MFMA_BM=0|1: tuning build override)
+  const int force_bm = tuning().mfma_bm;
+  g->bm = S <= 192 && kernel_path() != 2 && (force_bm == 1 || (force_bm == 2 && bm_auto(p)));
   // window row pitch: a workgroup's 8 blocks span 16 (tc1 - tc0) + 32 <= 16 (S / 8 + 8) + 32
   // bytes (<= 544 up to S = 192)
   g->bm_lp = S <= 64 ? 288 : 544;
@@ -1356,11 +1345,7 @@ bool plan_mfma_ssd(const SearchArgs& p, MfmaGeom* g) {
   // chunk rows L = P0 + 16 KM: fewest (chunks x (L + P0)) steps on an interior tile
   const int ny = min(48 + 2 * S + 1, H - 15);
   int best = 1 << 30;
-  static int force_km = -1;  // ME_MFMA_KM=2|3: tuning override, read once
-  if (force_km < 0) {
-    const char* e = getenv("ME_MFMA_KM");
-    force_km = e ? atoi(e) : 0;
-  }
+  const int force_km = tuning().mfma_km;  // ME_MFMA_KM=2|3: tuning build override
   for (int km = 2; km <= 3; km++) {  // km = 1 spills (its lone main-loop pass gets peeled)
     if (force_km && km != force_km) continue;
     const int L = 12 + ME_MFMA_DLY + 16 * km, ch = (ny + L - 1) / L;
@@ -1371,14 +1356,7 @@ bool plan_mfma_ssd(const SearchArgs& p, MfmaGeom* g) {
   // groups per workgroup: two when the tile needs an even number of groups
   // (whole tiles at 1080p +-32: no merge), else one (4K +-64: 3 workgroups)
   g->ngxw = ngx % 2 == 0 ? 2 : 1;
-  {
-    static int force_w = -1;  // ME_MFMA_NGXW=1|2: tuning override, read once
-    if (force_w < 0) {
-      const char* e = getenv("ME_MFMA_NGXW");
-      force_w = e ? atoi(e) : 0;
-    }
-    if (force_w == 1 || force_w == 2) g->ngxw = force_w;
-  }
+  if (tuning().mfma_ngxw) g->ngxw = tuning().mfma_ngxw;  // ME_MFMA_NGXW: tuning build
   if (!g->bm && (ngx + g->ngxw - 1) / g->ngxw > 1 &&
       (!p.mkeys || !p.mcnt || p.merge_tiles < mfma_merge_tiles(p)))
     return false;  // tiles span workgroups: needs the merge buffers

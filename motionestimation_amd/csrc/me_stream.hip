@@ -35,15 +35,7 @@ namespace {
 std::mutex g_pin_mu;
 std::map<uintptr_t, size_t> g_pinned;  // me_host_alloc ranges: base -> bytes
 // Freed frame slots kept cooling before reuse (ME_STREAM_COOL overrides; tuning)
-static int cooling_slots() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("ME_STREAM_COOL");
-    v = e ? atoi(e) : 2;
-    if (v < 1) v = 1;
-  }
-  return v;
-}
+static int cooling_slots() { return tuning().stream_cool > 0 ? tuning().stream_cool : 2; }
 }  // namespace
 
 bool host_range_pinned(const void* p, size_t bytes) {
@@ -185,11 +177,7 @@ me_status run_pairs(me_ctx* c, Dev& d, const Job& j, int p0, int p1) {
     for (int side = 0; side < 2; side++)
       all_pinned = all_pinned &&
                    host_range_pinned(j.frames[j.pairs[2 * n + side]], (size_t)(H - 1) * j.stride + W);
-  static int env_ahead = -1;  // ME_STREAM_AHEAD=1..8 (9+: unbounded, diagnostic), read once
-  if (env_ahead < 0) {
-    const char* e = getenv("ME_STREAM_AHEAD");
-    env_ahead = e ? atoi(e) : 0;
-  }
+  const int env_ahead = tuning().stream_ahead;  // tuning build: 1..8, 9 unbounded (diagnostic)
   const int kAhead = env_ahead > 8 ? 1 << 30 : env_ahead >= 1 ? env_ahead : (all_pinned ? 2 : 3);
   for (auto& e : d.pair_ev)
     if (!e) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -242,7 +230,7 @@ me_status run_pairs(me_ctx* c, Dev& d, const Job& j, int p0, int p1) {
       const me_status st = me::attach_scratch(c, d, p);
       if (st != ME_OK) return st;
     }
-    HIPCHK(c, me::launch_search(p, d.stream, nullptr));
+    if ((s = me::launch_ordered(c, d, p, d.stream)) != ME_OK) return s;
     if (kAhead <= 8) HIPCHK(c, hipEventRecord(d.pair_ev[(n - p0) % kAhead], d.stream));
     for (int side = 0; side < 2; side++) {
       const int f = j.pairs[2 * n + side];

@@ -1,0 +1,32 @@
+// me_tuning.h -- planner overrides for the tuning tools (internal).
+//
+// The default build (libme_hip.so) reads no environment beyond the documented
+// ME_PATH (include/me.h): tuning() returns the automatic settings.  The
+// diagnostic build libme_hip_tune.so (csrc/Makefile `tune`, -DME_TUNING in
+// me_api.hip only) parses the overrides below once per process, thread-safely,
+// and rejects malformed values with a message on stderr (the automatic setting
+// stays).  tools/plan_sweep.py, tools/dyn_sweep.sh and tools/dbg/* select it
+// with ME_HIP_LIB=libme_hip_tune.so.
+#pragma once
+
+namespace me {
+
+struct Tuning {
+  // ME_PLAN="K,tb,cpp,threads[,fold]": fast-kernel plan (0 = free; fold -1 = free)
+  int plan_k = 0, plan_tb = 0, plan_cpp = 0, plan_threads = 0, plan_fold = -1;
+  int dyn = -1;           // ME_DYN: tiles per workgroup for dynamic pulls (-1 = automatic)
+  int mfma_bm = 2;        // ME_MFMA_BM=0|1: block-major SSD kernel off / on (2 = automatic)
+  int mfma_km = 0;        // ME_MFMA_KM=2|3: 8x8/tile kernel chunk length (0 = automatic)
+  int mfma_ngxw = 0;      // ME_MFMA_NGXW=1|2: column groups per workgroup (0 = automatic)
+  int stream_cool = 0;    // ME_STREAM_COOL=1..64: cooling frame slots (0 = automatic)
+  int stream_ahead = 0;   // ME_STREAM_AHEAD=1..9: host run-ahead (9: unbounded; 0 = automatic)
+};
+
+const Tuning& tuning();
+
+// Kernel path (me_set_kernel_path / ME_PATH): 0 automatic, 1 VALU kernels only,
+// 2 no block-major MFMA kernel.  Atomic: read by planner threads.
+int kernel_path();
+void set_kernel_path_code(int v);
+
+}  // namespace me

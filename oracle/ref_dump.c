@@ -12,7 +12,10 @@
  * main.c is compiled with -Dmain=reference_main so its driver is not linked
  * as the entry point; nothing else in the reference is changed.
  *
- * usage: ref_dump <cur.yuv> <ref.yuv> <W> <H> <blk> <span> <out.bin>
+ * usage: ref_dump <cur.yuv> <ref.yuv> <W> <H> <blk> <span> <out.bin> [begin end]
+ * The optional raster block range [begin, end) lets a large frame (8K 8x8
+ * +-128: ~30 CPU-minutes) be dumped as parallel slabs that concatenate to the
+ * whole-frame record stream (tests/golden/make_golden.py --big).
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -24,8 +27,8 @@ float findBestBlkMse(predictionFrame pf, int* referenceFrame, block* blk,
                      int extraSpan);
 
 int main(int argc, char** argv) {
-  if (argc != 8) {
-    fprintf(stderr, "usage: ref_dump cur ref W H blk span out.bin\n");
+  if (argc != 8 && argc != 10) {
+    fprintf(stderr, "usage: ref_dump cur ref W H blk span out.bin [begin end]\n");
     return 2;
   }
   int W = atoi(argv[3]), H = atoi(argv[4]);
@@ -38,7 +41,13 @@ int main(int argc, char** argv) {
   createPredictionFrame(&p, cur, W, H, blk);
   FILE* f = fopen(argv[7], "wb");
   if (!f) return 1;
-  for (int i = 0; i < p.num_blks; i++) {
+  int begin = 0, end = p.num_blks;
+  if (argc == 10) {
+    begin = atoi(argv[8]);
+    end = atoi(argv[9]);
+    if (begin < 0 || end > p.num_blks || begin > end) return 2;
+  }
+  for (int i = begin; i < end; i++) {
     float mse = findBestBlkMse(p, ref, &p.blks[i], span);
     int rec[2] = {p.blks[i].motion_vectorX, p.blks[i].motion_vectorY};
     fwrite(rec, sizeof(int), 2, f);

@@ -18,17 +18,18 @@ GOLDEN = os.path.join(REPO, "tests", "golden")
 SSD, SAD, MSE_FLOAT, SSIM = 0, 1, 2, 3
 _KIND = {"ssd": SSD, "sad": SAD, "mse": MSE_FLOAT, "ssim": 3}
 
-_lib = None
+_libs = {}
 
 
 def build() -> None:
-    subprocess.run(["make", "-s", "-C", ORACLE_DIR, "liboracle.so", "me_cpu"], check=True)
+    subprocess.run(["make", "-s", "-C", ORACLE_DIR, "liboracle.so", "liboracle_O0.so", "me_cpu"],
+                   check=True)
 
 
-def lib():
-    global _lib
-    if _lib is None:
-        path = os.path.join(ORACLE_DIR, "liboracle.so")
+def lib(variant: str = ""):
+    """liboracle.so (-O2), or variant "O0": the same source built without optimisation."""
+    if variant not in _libs:
+        path = os.path.join(ORACLE_DIR, f"liboracle{'_' + variant if variant else ''}.so")
         if not os.path.exists(path):
             build()
         L = ctypes.CDLL(path)
@@ -46,8 +47,8 @@ def lib():
         L.orc_psnr.argtypes = [u8p, u8p, ctypes.c_int, ctypes.c_int]
         L.orc_psnr.restype = ctypes.c_double
         L.orc_now.restype = ctypes.c_double
-        _lib = L
-    return _lib
+        _libs[variant] = L
+    return _libs[variant]
 
 
 def _p(a, t):
@@ -62,7 +63,7 @@ def candidate_count(w, h, blk, span):
     return int(lib().orc_candidate_count(w, h, blk, span))
 
 
-def full_search(ref, cur, blk, span, cost="ssd", threads=None, begin=0, end=None):
+def full_search(ref, cur, blk, span, cost="ssd", threads=None, begin=0, end=None, variant=""):
     """Oracle full search on (H, W) uint8 planes.  Returns (mv[n,2] int16,
     cost[n] uint32, mse[n] float32) for blocks [begin, end)."""
     ref = np.ascontiguousarray(ref, np.uint8)
@@ -75,7 +76,7 @@ def full_search(ref, cur, blk, span, cost="ssd", threads=None, begin=0, end=None
     c = np.zeros(max(k, 1), np.uint32)
     m = np.zeros(max(k, 1), np.float32)
     threads = threads or os.cpu_count() or 1
-    rc = lib().orc_full_search(_p(ref, ctypes.c_uint8), _p(cur, ctypes.c_uint8), w, h, w, blk,
+    rc = lib(variant).orc_full_search(_p(ref, ctypes.c_uint8), _p(cur, ctypes.c_uint8), w, h, w, blk,
                                span, _KIND[cost], threads, begin, end,
                                _p(mv, ctypes.c_int16), _p(c, ctypes.c_uint32),
                                _p(m, ctypes.c_float))

@@ -1,0 +1,119 @@
+"""GPU: the context's one-search-at-a-time contract across streams, the
+multi-device path inside the library (row stripes + one RCCL ncclGather,
+csrc/me_api.hip multi_search), and bench.py's stripe mode end to end (the
+north_star's 8-GPU split: one frame in row stripes, one gather per frame).
+
+Tests that need two or more GPUs skip on a one-GPU box; the stripe-mode bench
+is also run here as a 2-rank gloo rehearsal on one GPU (each rank searches its
+stripe through libme_hip.so; the gather goes over gloo)."""
+import ctypes
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+import motionestimation_amd as me
+from motionestimation_amd import synth
+
+pytestmark = pytest.mark.gpu
+NT = min(16, os.cpu_count() or 1)
+
+
+def _ngpu():
+    import torch
+    return torch.cuda.device_count()
+
+
+def _resident(ref, cur, blk):
+    import torch
+    h, w = ref.shape
+    n = me.num_blocks(w, h, blk)
+    return (torch.from_numpy(ref).cuda(), torch.from_numpy(cur).cuda(),
+            torch.full((n, 2), -7, dtype=torch.int16, device="cuda"),
+            torch.zeros(n, dtype=torch.int32, device="cuda"))
+
+
+@pytest.mark.parametrize("cost,blk,span,w,h", [
+    ("ssd", 16, 32, 1920, 1080),   # MFMA path: shared prepass scratch
+    ("ssd", 8, 24, 1280, 720),     # 8x8 MFMA path: merge keys + tile counters
+    ("sad", 16, 16, 3840, 2160),   # qsad path with dynamic tile counters
+])
+def test_two_streams_one_context(cost, blk, span, w, h):
+    """Two searches of one context enqueued back to back on two streams: the
+    second waits for the first (they share the device's counters and scratch),
+    so both fields are exact."""
+    import torch
+    a_ref, a_cur = synth.frame_pair(w, h, 31, 3, -2)
+    b_ref, b_cur = synth.frame_pair(w, h, 32, -4, 5)
+    with me.Engine(devices=[0]) as eng:
+        s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+        for _ in range(2):  # and again, with the streams' order swapped
+            ka, kb = _resident(a_ref, a_cur, blk), _resident(b_ref, b_cur, blk)
+            torch.cuda.synchronize()
+            for (rt, ct, mv, co), s in ((ka, s1), (kb, s2)):  # back to back, no host sync
+                eng.full_search_device(rt, ct, blk, span, cost, mv, co,
+                                       stream=ctypes.c_void_p(s.cuda_stream))
+            torch.cuda.synchronize()
+            for (ref, cur), (_, _, mv, co) in (((a_ref, a_cur), ka), ((b_ref, b_cur), kb)):
+                omv, oco, _ = O.full_search(ref, cur, blk, span, cost, threads=NT)
+                np.testing.assert_array_equal(mv.cpu().numpy(), omv)
+                np.testing.assert_array_equal(co.cpu().numpy().view(np.uint32), oco)
+            s1, s2 = s2, s1
+
+
+@pytest.mark.skipif("_ngpu() < 2", reason="needs >= 2 GPUs (ncclCommInitAll + ncclGather)")
+def test_multi_device_context_rccl_gather():
+    """me_create over distinct devices 0..n-1: me_full_search stripes the frame
+    across them and gathers with one ncclGather (me_api.hip multi_search)."""
+    ref, cur = synth.frame_pair(1920, 1080, 7, 5, -3)
+    n = _ngpu()
+    for devs in sorted({2, n}):
+        with me.Engine(devices=list(range(devs))) as eng:
+            for cost, span in (("sad", 32), ("ssd", 32), ("sad", 7)):
+                mv, c = eng.full_search(ref, cur, 16, span, cost)
+                omv, oc, _ = O.full_search(ref, cur, 16, span, cost, threads=NT)
+                np.testing.assert_array_equal(mv, omv, err_msg=f"{devs} devices {cost} S{span}")
+                np.testing.assert_array_equal(c, oc)
+
+
+def _bench_ranks(nproc, backend, extra=()):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={nproc}", "--master-addr=127.0.0.1", "--master-port=29731",
+           os.path.join(O.REPO, "bench.py"), "--gpus", str(nproc), "--dist-backend", backend,
+           "--steps", "4", "--warmup", "1", "--no-cpu", "--no-ssd", "--no-stream", *extra]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+def _check_stripe_line(d, nproc):
+    assert d["n_gpus"] == nproc and d["scaling"] == "strong"
+    assert d["config"]["parallelism"] == f"stripe{nproc}"
+    assert d["stripe_gather_parity"] is True
+    assert d["stripe_4k"]["stripe_gather_parity"] is True
+    assert d["stripe_4k"]["parallelism"] == f"stripe{nproc}"
+    assert d["value"] > 0 and d["stripe_4k"]["value"] > 0
+
+
+def test_bench_stripe_mode_two_ranks_gloo_rehearsal():
+    """bench.py --gpus 2 in its N > 1 default (stripe mode) with two ranks on
+    one GPU over gloo: each rank's stripe goes through libme_hip.so and the
+    gathered 1080p and 4K fields equal a full-frame search."""
+    _check_stripe_line(_bench_ranks(2, "gloo"), 2)
+
+
+@pytest.mark.skipif("_ngpu() < 2", reason="needs >= 2 GPUs (one RCCL rank per GPU)")
+def test_bench_stripe_mode_rccl():
+    """The same over RCCL, one rank per GPU (asynchronous gathers overlapping
+    the next frame's search)."""
+    n = min(_ngpu(), 8)
+    _check_stripe_line(_bench_ranks(2, "nccl"), 2)
+    if n > 2:
+        _check_stripe_line(_bench_ranks(n, "nccl"), n)

@@ -134,3 +134,26 @@ def test_oracle_ssim_matches_reference_goldens(manifest):
         pos = gscore > 0
         np.testing.assert_array_equal(mv[pos].astype(np.int32), gmv[pos], err_msg=c["name"])
         assert (mv[~pos] == 0).all()  # defined as (0, 0) here
+
+
+def test_big_cases_pin_frames_and_oracle_band(manifest):
+    """The whole-frame hash pins (tests/golden/make_big_golden.py) refer to the
+    synth frames pinned here, and the SAD restatement reproduces band 0 of the
+    4K +-64 pin (the GPU tests check every band of every big case)."""
+    from motionestimation_amd import synth
+    names = {c["name"] for c in manifest["big_cases"]}
+    assert {"big_8k_b8_s128_ssd", "big_8k_b8_s128_sad", "big_4k_b16_s64_sad"} <= names
+    for cfg in ("4k", "8k"):
+        ref, cur = synth.named_pair(cfg)
+        for tag, arr in (("ref", ref), ("cur", cur)):
+            assert hashlib.sha256(arr.tobytes()).hexdigest() == \
+                manifest["frames"][f"synth:{cfg}:{tag}"]["sha256"], (cfg, tag)
+    case = [c for c in manifest["big_cases"] if c["name"] == "big_4k_b16_s64_sad"][0]
+    ref, cur = synth.named_pair("4k")
+    nbx, nby = 240, 135
+    r1 = nby // case["bands"]
+    mv, cost, _ = O.full_search(ref, cur, 16, 64, "sad", begin=0, end=r1 * nbx)
+    rec = np.empty((len(mv), 8), np.uint8)
+    rec[:, :4] = mv.view(np.uint8).reshape(-1, 4)
+    rec[:, 4:] = cost.view(np.uint8).reshape(-1, 4)
+    assert hashlib.sha256(rec.tobytes()).hexdigest() == case["band_sha256"][0]

@@ -32,7 +32,7 @@ def main():
     if a.plans:
         plans = ["auto"] + a.plans.split(";")
     for plan in plans:
-        env = dict(os.environ)
+        env = dict(os.environ, ME_HIP_LIB="libme_hip_tune.so")  # ME_PLAN: tuning build only
         if plan != "auto":
             env["ME_PLAN"] = plan
         r = subprocess.run([sys.executable, os.path.join(HERE, "size_sweep.py"), "--cost", a.cost,
