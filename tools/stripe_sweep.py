@@ -1,0 +1,71 @@
+"""Per-rank stripe search time on ONE GPU, for the N-GPU row-stripe split.
+
+For N in --ranks, plan the N candidate-balanced stripes (me_plan_stripes) of a
+BASELINE config and time every rank's stripe search (its halo-only planes,
+me_full_search_stripe_device) back to back on this GPU.  The slowest stripe is
+the compute-bound step time of the N-GPU strong-scaling run (the RCCL gather
+overlaps the next frame's search in bench.py's stripe mode), so
+t(N=1) / max_r t_r(N) is the compute-side speed-up ceiling.  One JSON line per N.
+
+  python tools/stripe_sweep.py [--config 1080p|4k|8k] [--cost sad] [--ranks 1,2,4,8]
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import motionestimation_amd as me  # noqa: E402
+from motionestimation_amd import shard, synth  # noqa: E402
+
+CONFIGS = {"1080p": ("1080p", 16, 32), "4k": ("4k", 16, 64), "8k": ("8k", 8, 128)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="1080p", choices=list(CONFIGS))
+    ap.add_argument("--cost", default="sad")
+    ap.add_argument("--ranks", default="1,2,4,8")
+    ap.add_argument("--iters", type=int, default=30)
+    a = ap.parse_args()
+    cfg, blk, span = CONFIGS[a.config]
+    w, h, seed, sx, sy = synth.CONFIGS[cfg]
+    ref, cur = synth.frame_pair(w, h, seed, sx, sy)
+    eng = me.Engine()
+    base = None
+    for n in [int(x) for x in a.ranks.split(",")]:
+        times = []
+        for st in shard.plan(w, h, blk, span, n):
+            if not st.nblocks:
+                times.append(0.0)
+                continue
+            rt = torch.from_numpy(ref[st.ref_y0:st.ref_y1].copy()).cuda()
+            ct = torch.from_numpy(cur[st.cur_y0:st.cur_y1].copy()).cuda()
+            mv = torch.empty((st.nblocks, 2), dtype=torch.int16, device="cuda")
+            co = torch.empty(st.nblocks, dtype=torch.int32, device="cuda")
+
+            def run():
+                eng.search_stripe_device(rt, st.ref_y0, ct, st.cur_y0, w, h, blk, span, a.cost,
+                                         st.row_begin, st.row_end, mv, co)
+            for _ in range(5):
+                run()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            e0.record()
+            for _ in range(a.iters):
+                run()
+            e1.record()
+            torch.cuda.synchronize()
+            times.append(e0.elapsed_time(e1) / a.iters)
+        t = max(times)
+        base = base or t
+        print(json.dumps({"config": a.config, "cost": a.cost, "ranks": n,
+                          "stripe_ms": [round(x, 4) for x in times], "max_ms": t,
+                          "compute_speedup_vs_1": base / t}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,9 +1,16 @@
 // valu_microbench.hip -- issue-rate microbenchmark for the integer ops the
-// block matcher can be built from (gfx950).  Each kernel runs 8 independent
-// accumulation chains of ONE instruction with loop-invariant operands (no
-// other VALU in the loop body), over the whole chip at 8 waves/SIMD, and
-// stamps s_memtime / s_memrealtime to report the clock the chip actually held.
-// Output: one JSON line per op with cycles per wave-instruction per SIMD.
+// block matcher can be built from (gfx950).
+//
+// Each kernel runs 8 independent chains of ONE instruction over the whole chip.
+// The instruction is emitted by `asm volatile` with its result fed back as an
+// operand (a loop-carried, data-dependent chain), so the compiler can neither
+// fold the loop (v_add / v_min: a builtin `acc += x` loop collapses to one
+// multiply) nor schedule anything else into it.  Rates are taken from the whole
+// launch: wave-instructions per second over the chip, and
+//     cycles per wave-instruction per SIMD = clock * SIMDs / (wave-instr/s)
+// with the clock the chip held (s_memtime / s_memrealtime) and SIMDs = 4 x CUs,
+// so the result does not depend on how many waves were resident at once.
+// Output: one JSON line per op.
 //
 // build: hipcc --offload-arch=gfx950 -O3 tools/valu_microbench.hip -o bin/valu_microbench
 #include <hip/hip_runtime.h>
@@ -13,9 +20,31 @@
 #define CHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
   fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); return 1; } } while (0)
 
-constexpr int ITERS = 1024;
-constexpr int UNROLL = 32;
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+constexpr int ITERS = 512;
+constexpr int UNROLL = 16;
+
+// One chain step of op OP: acc (32- or 64-bit) is both read and written.
+template <int OP>
+__device__ __forceinline__ void step(uint32_t& a, uint64_t& a64, uint32_t x, uint32_t y,
+                                     uint64_t x64, float& fa, float fx) {
+  if constexpr (OP == 0) asm volatile("v_add_u32 %0, %0, %1" : "+v"(a) : "v"(x));
+  if constexpr (OP == 1) asm volatile("v_sad_u8 %0, %1, %2, %0" : "+v"(a) : "v"(x), "v"(y));
+  if constexpr (OP == 2) asm volatile("v_qsad_pk_u16_u8 %0, %1, %2, %0" : "+v"(a64) : "v"(x64), "v"(y));
+  if constexpr (OP == 3) asm volatile("v_dot4_u32_u8 %0, %1, %2, %0" : "+v"(a) : "v"(x), "v"(y));
+  if constexpr (OP == 4) asm volatile("v_alignbyte_b32 %0, %0, %1, %2" : "+v"(a) : "v"(x), "v"(y));
+  if constexpr (OP == 5) asm volatile("v_fma_f32 %0, %0, %1, 0.5" : "+v"(fa) : "v"(fx));
+  if constexpr (OP == 6) asm volatile("v_sad_u16 %0, %1, %2, %0" : "+v"(a) : "v"(x), "v"(y));
+  if constexpr (OP == 7) asm volatile("v_perm_b32 %0, %0, %1, %2" : "+v"(a) : "v"(x), "v"(y));
+  if constexpr (OP == 8) asm volatile("v_min_u32 %0, %0, %1" : "+v"(a) : "v"(x));
+  if constexpr (OP == 9) asm volatile("v_min3_u32 %0, %0, %1, %2" : "+v"(a) : "v"(x), "v"(y));
+  if constexpr (OP == 10) asm volatile("v_lshl_or_b32 %0, %0, 16, %1" : "+v"(a) : "v"(x));
+  if constexpr (OP == 11) asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(a) : "v"(x));
+  if constexpr (OP == 12) asm volatile("v_mul_hi_u32 %0, %0, %1" : "+v"(a) : "v"(x));
+  if constexpr (OP == 13) asm volatile("v_pk_max_u16 %0, %0, %1" : "+v"(a) : "v"(x));
+  if constexpr (OP == 14) asm volatile("v_msad_u8 %0, %1, %2, %0" : "+v"(a) : "v"(x), "v"(y));
+  if constexpr (OP == 15) asm volatile("v_add_co_u32 %0, vcc, %0, %1" : "+v"(a) : "v"(x) : "vcc");
+  if constexpr (OP == 16) asm volatile("v_lshlrev_b64 %0, 1, %0" : "+v"(a64));
+}
 
 template <int OP>
 __global__ __launch_bounds__(256) void bench(const uint32_t* in, uint32_t* out, uint64_t* clk) {
@@ -30,30 +59,15 @@ __global__ __launch_bounds__(256) void bench(const uint32_t* in, uint32_t* out, 
     acc[i] = in[(l + 5 * i + 2) & 63];
     x64[i] = ((uint64_t)y[i] << 32) | x[i];
     acc64[i] = acc[i];
-    fx[i] = (float)x[i];
-    fa[i] = (float)acc[i];
+    fx[i] = (float)(x[i] >> 8) * 1e-7f;
+    fa[i] = (float)(acc[i] >> 8);
   }
   uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
   for (int it = 0; it < ITERS; it++) {
 #pragma unroll
     for (int u = 0; u < UNROLL; u++) {
 #pragma unroll
-      for (int i = 0; i < 8; i++) {
-        if constexpr (OP == 0) acc[i] = acc[i] + x[i];
-        if constexpr (OP == 1) acc[i] = __builtin_amdgcn_sad_u8(x[i], y[i], acc[i]);
-        if constexpr (OP == 2) acc64[i] = __builtin_amdgcn_qsad_pk_u16_u8(x64[i], y[i], acc64[i]);
-        if constexpr (OP == 3) acc[i] = __builtin_amdgcn_udot4(x[i], y[i], acc[i], false);
-        if constexpr (OP == 4) acc[i] = __builtin_amdgcn_alignbyte(acc[i], x[i], y[i]);
-        if constexpr (OP == 5) fa[i] = __builtin_fmaf(fa[i], fx[i], 0.5f);
-        if constexpr (OP == 6) acc[i] = __builtin_amdgcn_sad_u16(x[i], y[i], acc[i]);
-        if constexpr (OP == 7) acc[i] = __builtin_amdgcn_perm(acc[i], x[i], y[i]);
-        if constexpr (OP == 8) acc[i] = __builtin_amdgcn_udot4(x[i], x[i], acc[i], false) - acc[i];
-        if constexpr (OP == 9) acc[i] = min(acc[i], x[i]);
-        if constexpr (OP == 10) {
-          u32x4 v = __builtin_amdgcn_mqsad_u32_u8(x64[i], y[i], (u32x4){acc[i], x[i], y[i], acc[i]});
-          acc[i] = v[0];
-        }
-      }
+      for (int i = 0; i < 8; i++) step<OP>(acc[i], acc64[i], x[i], y[i], x64[i], fa[i], fx[i]);
     }
   }
   uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
@@ -69,7 +83,8 @@ __global__ __launch_bounds__(256) void bench(const uint32_t* in, uint32_t* out, 
 }
 
 template <int OP>
-static int run(const char* name, const uint32_t* d_in, uint32_t* d_out, uint64_t* d_clk, int blocks) {
+static int run(const char* name, const uint32_t* d_in, uint32_t* d_out, uint64_t* d_clk,
+               int blocks, int simds, int waves_per_simd = 0) {
   hipEvent_t e0, e1;
   CHK(hipEventCreate(&e0));
   CHK(hipEventCreate(&e1));
@@ -84,14 +99,15 @@ static int run(const char* name, const uint32_t* d_in, uint32_t* d_out, uint64_t
   CHK(hipEventElapsedTime(&ms, e0, e1));
   uint64_t c[3];
   CHK(hipMemcpy(c, d_clk, 24, hipMemcpyDeviceToHost));
-  double ghz = (double)c[0] / ((double)c[1] / 100e6) / 1e9;  // memrealtime = 100 MHz
-  double per_wave_instr = (double)ITERS * UNROLL * 8;
-  double cyc_per_wave = (double)c[0] / c[2];
-  // 8 waves per SIMD share the SIMD: cycles per wave-instruction per SIMD.
-  double cyc_per_instr_simd = cyc_per_wave / per_wave_instr / 8.0;
-  double winst = (double)blocks * 4 * per_wave_instr;
-  printf("{\"op\": \"%s\", \"ms\": %.3f, \"clock_ghz\": %.3f, \"cyc_per_wave_instr_per_simd\": %.3f, "
-         "\"wave_instr_per_s\": %.4g}\n", name, ms, ghz, cyc_per_instr_simd, winst / (ms / 1e3));
+  const double ghz = (double)c[0] / ((double)c[1] / 100e6) / 1e9;  // memrealtime = 100 MHz
+  const double per_wave = (double)ITERS * UNROLL * 8;
+  const double winst = (double)blocks * 4 * per_wave;
+  const double rate = winst / (ms / 1e3);                         // wave-instructions / s, chip
+  const double cyc = ghz * 1e9 * simds / rate;                    // per wave-instruction per SIMD
+  printf("{\"op\": \"%s\", \"ms\": %.3f, \"clock_ghz\": %.3f, \"cyc_per_wave_instr_per_simd\": %.2f, "
+         "\"wave_instr_per_s\": %.4g, \"simds\": %d", name, ms, ghz, cyc, rate, simds);
+  if (waves_per_simd) printf(", \"waves_per_simd\": %d", waves_per_simd);
+  printf("}\n");
   return 0;
 }
 
@@ -100,21 +116,40 @@ int main() {
   for (int i = 0; i < 64; i++) h[i] = 0x9E3779B9u * (i + 1);
   uint32_t *d_in, *d_out;
   uint64_t* d_clk;
+  int dev = 0, cus = 0;
+  CHK(hipGetDevice(&dev));
+  CHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   CHK(hipMalloc(&d_in, sizeof h));
   CHK(hipMalloc(&d_out, 64));
   CHK(hipMalloc(&d_clk, 24));
   CHK(hipMemcpy(d_in, h, sizeof h, hipMemcpyHostToDevice));
-  int blocks = 256 * 8;  // 8 WGs of 4 waves per CU = 8 waves per SIMD
-  run<0>("v_add_u32", d_in, d_out, d_clk, blocks);
-  run<5>("v_fma_f32", d_in, d_out, d_clk, blocks);
-  run<9>("v_min_u32", d_in, d_out, d_clk, blocks);
-  run<1>("v_sad_u8", d_in, d_out, d_clk, blocks);
-  run<6>("v_sad_u16", d_in, d_out, d_clk, blocks);
-  run<2>("v_qsad_pk_u16_u8", d_in, d_out, d_clk, blocks);
-  run<10>("v_mqsad_u32_u8", d_in, d_out, d_clk, blocks);
-  run<3>("v_dot4_u32_u8", d_in, d_out, d_clk, blocks);
-  run<8>("v_dot4_u32_u8+v_sub", d_in, d_out, d_clk, blocks);
-  run<4>("v_alignbyte_b32", d_in, d_out, d_clk, blocks);
-  run<7>("v_perm_b32", d_in, d_out, d_clk, blocks);
+  const int blocks = cus * 8;  // 8 waves per SIMD when resident; rates do not assume it
+  const int simds = 4 * cus;
+  run<5>("v_fma_f32", d_in, d_out, d_clk, blocks, simds);
+  run<0>("v_add_u32", d_in, d_out, d_clk, blocks, simds);
+  run<15>("v_add_co_u32", d_in, d_out, d_clk, blocks, simds);
+  run<8>("v_min_u32", d_in, d_out, d_clk, blocks, simds);
+  run<9>("v_min3_u32", d_in, d_out, d_clk, blocks, simds);
+  run<10>("v_lshl_or_b32", d_in, d_out, d_clk, blocks, simds);
+  run<13>("v_pk_max_u16", d_in, d_out, d_clk, blocks, simds);
+  run<16>("v_lshlrev_b64", d_in, d_out, d_clk, blocks, simds);
+  run<11>("v_mul_lo_u32", d_in, d_out, d_clk, blocks, simds);
+  run<12>("v_mul_hi_u32", d_in, d_out, d_clk, blocks, simds);
+  run<1>("v_sad_u8", d_in, d_out, d_clk, blocks, simds);
+  run<14>("v_msad_u8", d_in, d_out, d_clk, blocks, simds);
+  run<6>("v_sad_u16", d_in, d_out, d_clk, blocks, simds);
+  run<2>("v_qsad_pk_u16_u8", d_in, d_out, d_clk, blocks, simds);
+  run<3>("v_dot4_u32_u8", d_in, d_out, d_clk, blocks, simds);
+  run<4>("v_alignbyte_b32", d_in, d_out, d_clk, blocks, simds);
+  run<7>("v_perm_b32", d_in, d_out, d_clk, blocks, simds);
+  // Occupancy sweep: one 256-thread workgroup per CU puts one wave on each
+  // SIMD, so `cus * w` workgroups (one wave of the grid resident) give w waves
+  // per SIMD: what a SIMD sustains with that many waves to pick from.
+  for (int w : {1, 2, 4}) {
+    run<2>("v_qsad_pk_u16_u8", d_in, d_out, d_clk, cus * w, simds, w);
+    run<1>("v_sad_u8", d_in, d_out, d_clk, cus * w, simds, w);
+    run<9>("v_min3_u32", d_in, d_out, d_clk, cus * w, simds, w);
+    run<0>("v_add_u32", d_in, d_out, d_clk, cus * w, simds, w);
+  }
   return 0;
 }
