@@ -138,7 +138,11 @@ me_status me_full_search_stripe_device(me_ctx* ctx, const uint8_t* d_ref,
                                        void* stream);
 
 /* Balanced stripe plan: bounds[0..n_shards] block-row boundaries, each stripe
- * carrying about the same exact candidate count. */
+ * carrying about the same search cost.  The cost of a block row is its block
+ * count times (3 * (2S+1) + ny) / 4, ny = its exact candidate-row count: the
+ * kernels compute a clipped top / bottom block row at nearly the price of an
+ * interior one (whole dy chunks, one staged window per tile), so edge rows are
+ * discounted by a quarter of their candidate deficit, not all of it. */
 me_status me_plan_stripes(int width, int height, int block_size,
                           int search_range, int n_shards, int* bounds);
 

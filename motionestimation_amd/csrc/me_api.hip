@@ -397,8 +397,21 @@ uint64_t me_candidate_count(int width, int height, int blk, int range) {
 me_status me_plan_stripes(int width, int height, int blk, int range, int n, int* bounds) {
   if (!bounds || n < 1 || width <= 0 || height <= 0 || blk <= 0 || range < 0) return ME_EINVAL;
   const int nby = (height + blk - 1) / blk;
+  // Row cost (include/me.h): nbx * (3 (2S + 1) + ny) -- an exact-candidate
+  // balance gave the 4K +-64 edge stripes 18 block rows against 16-17 inside,
+  // and 2,160 two-block tiles take three rounds of the chip's 1,024 workgroup
+  // slots where 2,040 take two (8-way 4K edge stripe 0.200 vs 0.153 ms,
+  // profiles/r02i_stripe_4k.jsonl).
   std::vector<uint64_t> cum(nby + 1, 0);
-  for (int by = 0; by < nby; by++) cum[by + 1] = cum[by] + row_candidates(width, height, blk, range, by);
+  const uint64_t nbx = (uint64_t)((width + blk - 1) / blk);
+  for (int by = 0; by < nby; by++) {
+    const int tly = by * blk;
+    const int h = height - tly < blk ? height - tly : blk;
+    const int dymin = -range > -tly ? -range : -tly;
+    const int dymax = range < height - h - tly ? range : height - h - tly;
+    const uint64_t ny = (uint64_t)(dymax - dymin + 1);
+    cum[by + 1] = cum[by] + nbx * (3 * (uint64_t)(2 * range + 1) + ny);
+  }
   bounds[0] = 0;
   int r = 0;
   for (int i = 1; i < n; i++) {

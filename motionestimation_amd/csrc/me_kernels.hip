@@ -858,6 +858,11 @@ bool plan_fast(const SearchArgs& p, QsadGeom* g, int* k_out) {
       const double wave_align = (64 % G == 0 || G % 64 == 0) ? 1.03 : 1.0;
       for (int tb = 1; tb <= 16; tb++) {
         if (force[1] && tb != force[1]) continue;
+        // One-block tiles restage a whole window per block and leave waves of
+        // every item part empty: measured slower than two-block tiles wherever
+        // both fit (1080p: 171 vs 121 us static; 4K block rows 0..17, the edge
+        // stripe of an 8-way split: 0.228 vs 0.188 ms; profiles/r02h_dyn.jsonl).
+        if (tb == 1 && !force[1] && g->nbx_full >= 2) continue;
         // bytes the lanes touch per row (+ a <= 3, + alignment word)
         const int width = (tb - 1) * B + (sad ? 4 * G + B + 4 : 2 * S + 1 + 3 + B + 4);
         int pt = (width + 15) & ~15;
@@ -916,6 +921,10 @@ bool plan_fast(const SearchArgs& p, QsadGeom* g, int* k_out) {
     // start items in lockstep and the item-start pulls serialise on the
     // device-scope counters while wave 0 waits.
     g->dyn_tiles = dyn_env >= 0 ? dyn_env : 3;
+    // ... and only for tiles of >= 16 wave-tasks: small tiles pay the pull per
+    // few tasks (1080p tb = 2: 184 vs 121 us static; profiles/r02h_dyn.jsonl).
+    const long tile_lanes = (long)bTB * bG * ((D + bK - 1) / bK);
+    if (dyn_env < 0 && tile_lanes < 16L * 64) g->dyn_tiles = 0;
   }
   g->tb = bTB;
   g->cpp = bC;

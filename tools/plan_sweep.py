@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--fold", default="-1")
     ap.add_argument("--plans", default="", help="explicit 'K,tb,cpp,thr,fold;...' (overrides the grid)")
     ap.add_argument("--iters", type=int, default=30)
+    ap.add_argument("--rows", default="", help="block rows r0:r1 (one row stripe)")
     a = ap.parse_args()
     plans = ["auto"] + [f"{k},{t},{c},{n},{f}" for k, t, c, n, f in itertools.product(
         a.K.split(","), a.tb.split(","), a.cpp.split(","), a.threads.split(","),
@@ -37,7 +38,8 @@ def main():
             env["ME_PLAN"] = plan
         r = subprocess.run([sys.executable, os.path.join(HERE, "size_sweep.py"), "--cost", a.cost,
                             "--blk", str(a.blk), "--span", str(a.span), "--width", str(a.width),
-                            "--heights", str(a.height), "--iters", str(a.iters)],
+                            "--heights", str(a.height), "--iters", str(a.iters)] +
+                           (["--rows", a.rows] if a.rows else []),
                            env=env, capture_output=True, text=True, timeout=300)
         line = [l for l in r.stdout.splitlines() if l.startswith("{")]
         if r.returncode != 0 or not line:
