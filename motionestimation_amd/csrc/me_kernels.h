@@ -55,6 +55,7 @@ struct QsadGeom {
   int wg_per_row;  // workgroups per block row
   int nbx_full;    // full-width blocks per row
   int aligned;     // 4-byte aligned global rows
+  int tile16;      // ref tile staged in 16-byte granules (X0, width, rows 16-byte aligned)
   int fold;        // SAD, S % 4 == 0: groups = S/2 cover dx in [-S, S-1]; the dx = +S
                    // column is spread over lanes gi < K, one v_sad_u8 candidate each
   int dyn_tiles;   // dynamic tile pulls when tiles >= dyn_tiles * workgroups (0: never)

@@ -490,10 +490,16 @@ __device__ __forceinline__ void stage_item(const SearchArgs& p, const QsadGeom& 
   if (g.aligned) {
     // tile byte (r, x) <- ref(prow0 + r, X0 + x); zeros outside the resident rows.
     const int base = (it.prow0 - p.ref_row0) * stride + it.X0;
-    dma4(rref, tile, it.prows * pitch, [&](int d) {
+    auto src = [&](int d) {
       const int r = (int)__umulhi((uint32_t)d, g.pitch_magic), x = d - r * pitch;
       return (uint32_t)(base + r * stride + x);
-    });
+    };
+    // 16-byte granules when X0, the frame width and the rows are 16-aligned:
+    // no granule straddles x = 0 or x = W, and a quarter of the DMA steps.
+    if (g.tile16)
+      dma16(rref, tile, it.prows * pitch, src);
+    else
+      dma4(rref, tile, it.prows * pitch, src);
     // cur block b, row oy -> LDS bytes (b * B + oy) * B
     const int cbase = (it.tly - p.cur_row0) * stride + it.bx0 * B;
     if constexpr (B == 16) {
@@ -946,6 +952,11 @@ bool plan_fast(const SearchArgs& p, QsadGeom* g, int* k_out) {
     if ((uint32_t)(((uint64_t)d * g->pitch_magic) >> 32) != d / (uint32_t)g->pitch) return false;
   g->wg_per_row = (g->nbx_full + g->tb - 1) / g->tb;
   g->aligned = (p.stride % 4 == 0) && ((uintptr_t)p.ref % 4 == 0) && ((uintptr_t)p.cur % 4 == 0);
+  // X0 = tb*B*t - S - a is 16-aligned for every tile when a = 0 (S % 4 == 0),
+  // S % 16 == 0 and tb * B % 16 == 0; rows of the ref plane 16-aligned; W % 16
+  // == 0 keeps the last in-frame granule of the last row inside the range.
+  g->tile16 = g->aligned && S % 16 == 0 && (g->tb * B) % 16 == 0 && p.width % 16 == 0 &&
+              p.stride % 16 == 0 && (uintptr_t)p.ref % 16 == 0;
   // umulhi(t, magic_groups) == t / groups for every task index of an item.
   g->magic_groups = 0xFFFFFFFFu / (uint32_t)g->groups + 1u;
   const uint32_t tmax = (uint32_t)(g->tb * g->groups * g->cpp);
@@ -1012,7 +1023,7 @@ hipError_t launch_fast(const SearchArgs& p, QsadGeom g, int K, int row0, int nro
 // Plans depend only on the search shape: cache them (per host thread) so a
 // steady stream of same-shape searches pays the planner once.
 struct PlanKey {
-  int width, height, stride, blk, range, cost, rows, aligned;
+  int width, height, stride, blk, range, cost, rows, aligned;  // aligned: 1 (4 B) | 2 (16 B)
   bool operator==(const PlanKey& o) const {
     return width == o.width && height == o.height && stride == o.stride && blk == o.blk &&
            range == o.range && cost == o.cost && rows == o.rows && aligned == o.aligned;
@@ -1030,7 +1041,8 @@ static bool cached_plan(const SearchArgs& p, QsadGeom* g, int* K) {
   thread_local PlanEntry cache[N];
   thread_local int used = 0, next = 0;
   const int aligned =
-      (p.stride % 4 == 0) && ((uintptr_t)p.ref % 4 == 0) && ((uintptr_t)p.cur % 4 == 0);
+      ((p.stride % 4 == 0) && ((uintptr_t)p.ref % 4 == 0) && ((uintptr_t)p.cur % 4 == 0)) |
+      (((p.stride % 16 == 0) && ((uintptr_t)p.ref % 16 == 0)) << 1);
   const PlanKey key{p.width, p.height, p.stride, p.blk, p.range, p.cost_kind,
                     p.block_row_end - p.block_row_begin, aligned};
   for (int i = 0; i < used; i++)
