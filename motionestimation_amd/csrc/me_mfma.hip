@@ -56,8 +56,11 @@
 #ifndef ME_SSD8_KM
 #define ME_SSD8_KM 3  // 8x8 chunk length L = 16 KM: 48 rows (8K +-128: 64 rows 7.12 ms, 48 6.95-7.0, 32 8.3)
 #endif
+#ifndef SSD8_STRIP
+#define SSD8_STRIP 32  // 8x8 kernel: tile columns per strip of the workgroup order (1,024 pixels)
+#endif
 #ifndef ME_SSD8_WP
-#define ME_SSD8_WP 80  // 8x8 window copy pitch: 4 x 72 x 80 + S2 table = 40 KB, four workgroups per CU
+#define ME_SSD8_WP 80  // 8x8 window copy pitch: 4 x (L + 8 = 56) x 80 + S2 table (L + 1) x 256 = 30 KB at L = 48
 #endif
 #ifndef ME_MFMA_ABLATE
 #define ME_MFMA_ABLATE 0  // diagnostic bit set (csrc/Makefile mablate, tools/mablate.sh); never shipped
@@ -686,11 +689,23 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd8_kernel(SearchArgs p, M
   const int wpt = g.ngx;  // one group per workgroup
   int tile, gx;
   {
+    // Workgroups in vertical strips of SSD8_STRIP tile columns, each strip
+    // walked down its tile rows (then across the strip, then the groups); each
+    // XCD (bid % 8, a speed heuristic only) takes one contiguous run of that
+    // order, so its L2 sweeps one strip top to bottom: a window / S2 row stays
+    // resident while the 9 tile rows that read it pass (tile-row-major order
+    // re-fetched it once per tile row: 8K +-128 1.56 GB per launch).
     const int nwg = (int)gridDim.x, bid = (int)blockIdx.x;
     const int x = bid & 7, m = bid >> 3, q = nwg >> 3, rem = nwg & 7;
     const int lin = x * q + min(x, rem) + m;
-    tile = lin / wpt;
-    gx = lin - tile * wpt;
+    const int sw = min(SSD8_STRIP, g.tiles_x);
+    const int per_strip = g.tiles_y * sw * wpt;
+    const int st = lin / per_strip, r = lin - st * per_strip;
+    const int sws = min(sw, g.tiles_x - st * sw);  // the last strip may be narrower
+    const int ty = r / (sws * wpt), r2 = r - ty * (sws * wpt);
+    const int txl = r2 / wpt;
+    gx = r2 - txl * wpt;
+    tile = ty * g.tiles_x + st * sw + txl;
   }
   const int tx = tile % g.tiles_x, ty = tile / g.tiles_x;
   const int bc0 = 4 * tx, br0 = g.row0 + 4 * ty;
@@ -1209,7 +1224,7 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_bm16_kernel(SearchArgs p, M
         };
         if constexpr (da) keys_of(accA, bA, i0A, i1A, 0, std::integral_constant<bool, ma == 3>{});
         if constexpr (db) keys_of(accB, bB, i0B, i1B, 2, std::integral_constant<bool, mb == 3>{});
-        if ((rel & 15) == 15 && i < iu1) widen(rel >> 4);  // S > 56: a band spans > 16 tiles
+        if ((rel & 15) == 15 && i < iu1) widen(rel >> 4);  // S >= 113: a band spans > 16 tiles
       };
       using T_ = std::true_type;
       using F_ = std::false_type;

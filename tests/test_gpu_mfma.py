@@ -77,6 +77,23 @@ def test_mfma_extreme_values(engine):
             _check(engine, ref, cur, span, f"{tag} S{span}")
 
 
+@pytest.mark.parametrize("span", [113, 128, 192])
+def test_mfma_extreme_values_segmented_bands(engine, span):
+    """The block-major kernel splits a band into 16-tile key segments from
+    S = 113 on (16 + 2S >= 256 positions): equal costs in two segments must
+    resolve to the raster-first (dy, dx).  All-ties and saturated planes on a
+    frame wide and tall enough for interior block pairs (40 blocks + 2S)."""
+    h, w = 16 * 6 + 2 * span, 16 * 40 + 2 * span
+    zeros, full = np.zeros((h, w), np.uint8), np.full((h, w), 255, np.uint8)
+    rng = np.random.default_rng(span)
+    binary = (rng.integers(0, 2, (h, w)) * 255).astype(np.uint8)
+    stripes = np.tile(((np.arange(w) // 2) % 2 * 200 + 20).astype(np.uint8), (h, 1))
+    for tag, ref, cur in [("flat", full, full), ("zeros", zeros, zeros), ("max", zeros, full),
+                          ("stripes", stripes, np.roll(stripes, 1, axis=1)),
+                          ("binary", binary, np.roll(binary, 5, axis=0))]:
+        _check(engine, ref, cur, span, f"{tag} S{span} {h}x{w}")
+
+
 def test_mfma_partial_edges_and_stride(engine):
     """Partial right column / bottom row (VALU kernels beside the MFMA tiles)
     and a row pitch larger than the width."""
@@ -180,12 +197,12 @@ def test_mfma8_8k_s128_sampled(engine):
 def test_mfma_random_shapes(engine):
     """Seeded random frame sizes, ranges and block sizes on every MFMA kernel
     (block-major, 4x4-block tiles, 8x8) and their edge paths, against the
-    oracle: widths/heights not multiples of B, ranges from 1 to 103, noise and
+    oracle: widths/heights not multiples of B, ranges from 1 to 192 (B = 16; 79 for B = 8), noise and
     smooth content."""
     rng = np.random.default_rng(4242)
     for it in range(150):
         blk = int(rng.choice([8, 16]))
-        span = int(rng.integers(1, 104 if blk == 16 else 80))
+        span = int(rng.integers(1, 193 if blk == 16 else 80))
         h = int(rng.integers(blk, 200))
         w = int(rng.integers(blk, 260))
         if rng.random() < 0.5:
