@@ -61,6 +61,7 @@ static Tuning read_tuning() {
   env_int("ME_MFMA_NGXW", 1, 2, &t.mfma_ngxw);
   env_int("ME_STREAM_COOL", 1, 64, &t.stream_cool);
   env_int("ME_STREAM_AHEAD", 1, 9, &t.stream_ahead);
+  env_int("ME_FLOW", 0, 1, &t.flow);
   return t;
 }
 const Tuning& tuning() {

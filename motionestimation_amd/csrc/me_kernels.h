@@ -59,6 +59,7 @@ struct QsadGeom {
   int fold;        // SAD, S % 4 == 0: groups = S/2 cover dx in [-S, S-1]; the dx = +S
                    // column is spread over lanes gi < K, one v_sad_u8 candidate each
   int dyn_tiles;   // dynamic tile pulls when tiles >= dyn_tiles * workgroups (0: never)
+  int flow_slots;  // me_flow_kernel: LDS ring slots (0: the persistent item kernel)
 };
 
 // Matrix-core SSD path (me_mfma.hip): B = 16, full-height rows [row0, row0 +

@@ -791,6 +791,247 @@ __global__ __launch_bounds__(1024) void me_fast_kernel(SearchArgs p, QsadGeom g)
 #endif
 }
 
+// --------------------------------------------------------------- flow (SAD)
+// One workgroup per CU, 16 waves, no barriers after the start.  The
+// workgroup's items (tiles of tb blocks with ALL their dy chunks) sit in a
+// ring of NB LDS slots; the waves pull wave-tasks (64 consecutive lane-tasks
+// of one item) from one LDS counter, so the 4 waves of every SIMD keep taking
+// work until the workgroup's list is empty: no item barrier, no per-item
+// partial last round of the workgroup (tb * G * chunks is a multiple of 64 on
+// the shapes the planner gives this kernel: 1080p +-32 tb = 4 -> 320 lanes).
+// The wave that finishes an item's last wave-task writes its blocks' vectors,
+// then refills the slot with item k + NB (LDS DMA, its own vmcnt wait) and
+// publishes it; a wave that pulls a task of an unpublished item sleeps on the
+// slot's ready word.  Pulls are in order, so the items < k are all pulled
+// before a wave waits on item k: the last of them to finish refills slot k % NB.
+struct FlowCtl {
+  uint32_t next;       // wave-tasks handed out
+  uint32_t ready[16];  // item index + 1 published in the slot
+  uint32_t done[16];   // wave-tasks of the slot's item finished
+};
+
+// Single-wave LDS DMA of one item (the aligned path): tile rows and cur blocks.
+template <int B>
+__device__ __forceinline__ void stage_item_wave(const SearchArgs& p, const QsadGeom& g, const Item& it,
+                                                uint8_t* buf, __amdgpu_buffer_rsrc_t rref,
+                                                __amdgpu_buffer_rsrc_t rcur) {
+  // lane recomputed per call (fresh_tid): hoisted lane-derived offsets spilled
+  const int lane = fresh_tid() & 63;
+  uint8_t* tile = buf;
+  uint8_t* cur = buf + g.tile_bytes;
+  const int pitch = g.pitch, stride = p.stride;
+  const int base = (it.prow0 - p.ref_row0) * stride + it.X0;
+  const int bytes = it.prows * pitch;
+  for (int s0 = 0; s0 < bytes; s0 += 1024) {  // 16-byte granules (g.tile16)
+    const int d = s0 + 16 * lane;
+    const int r = (int)__umulhi((uint32_t)d, g.pitch_magic), x = d - r * pitch;
+    if (d < bytes)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rref, (__attribute__((address_space(3))) void*)(tile + s0), 16,
+          (uint32_t)(base + r * stride + x), 0, 0, 0);
+  }
+  const int cbase = (it.tly - p.cur_row0) * stride + it.bx0 * B;
+  const int cb = it.nb * B * B;
+  for (int s0 = 0; s0 < cb; s0 += 1024) {
+    const int d = s0 + 16 * lane;
+    if (d < cb)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rcur, (__attribute__((address_space(3))) void*)(cur + s0), 16,
+          (uint32_t)(cbase + ((d >> 4) & 15) * stride + (d >> 8) * B), 0, 0, 0);
+  }
+}
+
+// Wave-tasks of one item: its lane-tasks (valid chunks x blocks x groups) / 64, rounded up.
+template <int B, int K>
+__device__ __forceinline__ int flow_tasks(const SearchArgs& p, const QsadGeom& g, const Item& it,
+                                          int* lc0_out) {
+  const int S = p.range;
+  const int dymin = max(-S, -it.tly), dymax = min(S, p.height - it.h - it.tly);
+  const int lc0 = max(0, (dymin + S) / K), lc1 = min(it.nch, (dymax + S) / K + 1);
+  *lc0_out = lc0;
+  return ((lc1 - lc0) * it.nb * g.groups + 63) >> 6;
+}
+
+template <int B, int K>
+__global__ __launch_bounds__(1024) void me_flow_kernel(SearchArgs p, QsadGeom g) {
+  static_assert(B == 16, "cur-block DMA layout of stage_item_wave");
+  constexpr int CW = B / 4;
+  extern __shared__ __align__(16) uint8_t smem[];
+  const int NB = g.flow_slots;
+  const int slot_bytes = g.tile_bytes + g.tb * B * B;
+  uint64_t* keys = reinterpret_cast<uint64_t*>(smem + NB * slot_bytes);  // [NB][tb]
+  FlowCtl* ctl = reinterpret_cast<FlowCtl*>(smem + NB * slot_bytes + NB * g.tb * 8);
+  const int tid = (int)threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int S = p.range;
+  const __amdgpu_buffer_rsrc_t rref =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.ref, (short)0, p.ref_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rcur =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.cur, (short)0, p.cur_bytes, 0x00020000);
+
+  // This workgroup's tiles: the XCD band of bid % 8 (a speed heuristic only),
+  // member m takes tiles band0 + m, + n_x, ...
+  const int ntiles = g.wg_per_row * g.nrows;
+  const int nwg = (int)gridDim.x, bid = (int)blockIdx.x;
+  const int ng = nwg < 8 ? nwg : 8;
+  const int x = bid % ng, m = bid / ng;
+  const int n_x = nwg / ng + (x < nwg % ng ? 1 : 0);
+  const int band0 = (int)((long)ntiles * x / ng), band1 = (int)((long)ntiles * (x + 1) / ng);
+  const int nitems = band1 - band0 > m ? (band1 - band0 - m + n_x - 1) / n_x : 0;
+  auto tile_of = [&](int k) { return band0 + m + k * n_x; };
+
+  if (tid < 64) {
+    if (tid == 0) ctl->next = 0;
+    if (tid < 16) {
+      ctl->ready[tid] = 0;
+      ctl->done[tid] = 0;
+    }
+  }
+  for (int i = tid; i < NB * g.tb; i += (int)blockDim.x) keys[i] = ~0ull;
+  __syncthreads();
+  // wave w < NB stages item w and publishes it
+  if (wave < NB && wave < nitems) {
+    stage_item_wave<B>(p, g, item_of<B, K>(p, g, tile_of(wave), 0), smem + wave * slot_bytes, rref,
+                       rcur);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0)
+      __hip_atomic_store(&ctl->ready[wave], (uint32_t)wave + 1u, __ATOMIC_RELEASE,
+                         __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+
+  int kc = 0, basec = 0, lc0c = 0, nwc = 0;  // this wave's view: item kc's first task, task count
+  Item itc;
+  bool have = false;
+  for (;;) {
+    uint32_t q = 0;
+    if (lane == 0) q = __hip_atomic_fetch_add(&ctl->next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    q = (uint32_t)__builtin_amdgcn_readfirstlane((int)q);
+    // advance to the item holding task q (pulls are in order: kc only grows)
+    if (!have && kc < nitems) {
+      itc = item_of<B, K>(p, g, tile_of(kc), 0);
+      nwc = flow_tasks<B, K>(p, g, itc, &lc0c);
+      have = true;
+    }
+    while (kc < nitems && (int)q >= basec + nwc) {
+      basec += nwc;
+      kc++;
+      if (kc < nitems) {
+        itc = item_of<B, K>(p, g, tile_of(kc), 0);
+        nwc = flow_tasks<B, K>(p, g, itc, &lc0c);
+      }
+    }
+    if (kc >= nitems) break;
+    const int slot = kc % NB;
+    // Bounded wait (the ordering argument above says it ends; the bound keeps a
+    // broken invariant from hanging the GPU: the search would then be wrong,
+    // which every parity test catches, instead of never finishing).
+    int spins = 0;
+    while (__hip_atomic_load(&ctl->ready[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) !=
+               (uint32_t)kc + 1u &&
+           ++spins < (1 << 20))
+      __builtin_amdgcn_s_sleep(2);
+    if (spins >= (1 << 20)) break;
+    const Item& it = itc;
+    uint8_t* buf = smem + slot * slot_bytes;
+    const uint32_t* cur_lds = reinterpret_cast<const uint32_t*>(buf + g.tile_bytes);
+    const uint32_t tile_off = (uint32_t)(slot * slot_bytes);
+    const int G = g.groups;
+    const int t = (int)q - basec;
+    const int i = 64 * t + lane;
+    const int T = nwc * 64;  // lanes past the item's tasks are masked below
+    const int dymin = max(-S, -it.tly), dymax = min(S, p.height - it.h - it.tly);
+    const int lc1 = min(it.nch, (dymax + S) / K + 1);
+    const int valid_lanes = (lc1 - lc0c) * it.nb * G;
+    const bool live = i < valid_lanes;
+    (void)T;
+    const int ii = live ? i : 0;
+    const int bg = (int)__umulhi((uint32_t)ii, g.magic_groups);  // ii / G
+    const int gi = ii - bg * G;
+    const uint32_t magic_nb = 0xFFFFFFFFu / (uint32_t)it.nb + 1u;
+    const int lcr = it.nb == 1 ? bg : (int)__umulhi((uint32_t)bg, magic_nb);
+    const int b = bg - lcr * it.nb;
+    const int lc = lc0c + lcr;
+    const int d0 = lc * K;
+    const int tlx = (it.bx0 + b) * B;
+    uint32_t c[B][CW];
+#pragma unroll
+    for (int y = 0; y < B; y++) {
+      if constexpr (CW == 4) {
+        const uint4 v = reinterpret_cast<const uint4*>(cur_lds)[b * B + y];
+        c[y][0] = v.x; c[y][1] = v.y; c[y][2] = v.z; c[y][3] = v.w;
+      } else {
+        const uint2 v = reinterpret_cast<const uint2*>(cur_lds)[b * B + y];
+        c[y][0] = v.x; c[y][1] = v.y;
+      }
+    }
+    const int dxmin = max(-S, -tlx), dxmax = min(S, p.width - B - tlx);
+    const int jlo = dymin + S - d0, jhi = dymax + S - d0;
+    const bool full_rows = dymin + S <= 0 && dymax + S >= it.nch * K - 1;
+    const int w0 = (b * B) / 4 + gi;
+    uint64_t acc[K];
+    const int jt = gi < K ? gi : K - 1;
+    const uint32_t toff = tile_off + (uint32_t)((lc * K + jt) * g.pitch + b * B + 2 * S);
+    uint32_t tsad = 0;
+    if (it.h == B) {
+      qsad_lane<B, K, B>(smem, g.pitch, tile_off, lc * K, w0, c, acc);
+      if (g.fold) tsad = tail_sad<B, B>(smem, g.pitch, toff, c);
+    } else {
+      qsad_lane<B, K, B / 2>(smem, g.pitch, tile_off, lc * K, w0, c, acc);
+      if (g.fold) tsad = tail_sad<B, B / 2>(smem, g.pitch, toff, c);
+    }
+    const int dxg = 4 * gi - S - it.a;
+    const bool edge = dxg < dxmin || dxg + 3 > dxmax || !live;
+    uint32_t best;
+    if (full_rows && __builtin_amdgcn_ballot_w64(edge) == 0) {
+      best = lane_best<K, false>(acc, 0u, 0u, jlo, jhi);
+    } else {
+      uint32_t mlo = 0, mhi = 0;
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const int dx = dxg + k;
+        const uint32_t msk = (dx < dxmin || dx > dxmax) ? 0xFFFFu : 0u;
+        if (k < 2) mlo |= msk << (16 * k);
+        else mhi |= msk << (16 * (k - 2));
+      }
+      best = lane_best<K, true>(acc, mlo, mhi, jlo, jhi);
+    }
+    if (g.fold) {
+      const bool tv = gi < K && jt >= jlo && jt <= jhi && S <= dxmax;
+      best = min(best, tv ? (tsad << 16) | (uint32_t)(5 * jt + 4) : ~0u);
+    }
+    if (live && best < 0xFFFF0000u) {
+      const int idx = (int)(best & 0xFFFFu), jj = idx / 5, k5 = idx - 5 * jj;
+      const int dy = d0 + jj - S, dx = k5 == 4 ? S : 4 * gi + k5 - S - it.a;
+      atomicMin(reinterpret_cast<unsigned long long*>(&keys[slot * g.tb + b]),
+                (unsigned long long)make_key(best >> 16, dx, dy));
+    }
+    // this wave-task is done; the last one of the item writes and refills the slot
+    uint32_t prev = 0;
+    if (lane == 0)
+      prev = __hip_atomic_fetch_add(&ctl->done[slot], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+    prev = (uint32_t)__builtin_amdgcn_readfirstlane((int)prev);
+    if ((int)prev + 1 == nwc) {
+      if (lane < it.nb) {
+        const uint64_t kk = keys[slot * g.tb + lane];
+        keys[slot * g.tb + lane] = ~0ull;
+        const int out = (it.by - p.block_row_begin) * p.nbx + it.bx0 + lane;
+        p.mv[2 * out] = (int16_t)((int)(kk & 0xFFFF) - 32768);
+        p.mv[2 * out + 1] = (int16_t)((int)((kk >> 16) & 0xFFFF) - 32768);
+        if (p.cost) p.cost[out] = (uint32_t)(kk >> 32);
+      }
+      if (lane == 0) __hip_atomic_store(&ctl->done[slot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      const int kn = kc + NB;
+      if (kn < nitems) {
+        stage_item_wave<B>(p, g, item_of<B, K>(p, g, tile_of(kn), 0), buf, rref, rcur);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0)
+          __hip_atomic_store(&ctl->ready[slot], (uint32_t)kn + 1u, __ATOMIC_RELEASE,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------ launch
 static int generic_lds_bytes(const SearchArgs& p, int* win_bytes) {
   const int B = p.blk;
@@ -971,6 +1212,90 @@ bool plan_fast(const SearchArgs& p, QsadGeom* g, int* k_out) {
   return true;
 }
 
+// The flow kernel (SAD, 16x16, S = 32, one 1,024-thread workgroup per CU): tiles of tb
+// blocks with all their dy chunks, tb * G * chunks a multiple of 64 (every
+// wave-task full), a ring of >= 4 slots in LDS, the ref tile in 16-byte
+// granules, and >= 2 tiles per CU (fewer leave most of the 16 waves idle: the
+// persistent item kernel takes small stripes).
+static constexpr int FLOW_K = 13;
+static constexpr int FLOW_LDS = 160 * 1024 - 1024;
+
+static int cu_count();
+
+bool plan_flow(const SearchArgs& p, QsadGeom* g) {
+  const int B = p.blk, S = p.range;
+  if (p.cost_kind != COST_SAD || B != 16) return false;
+  // fold (S % 8) and 16-byte tile granules (S % 16).  S <= 32: at 4K +-64 the
+  // item kernel's items are already whole waves (8 blocks x 4 chunks x 32
+  // groups) and it measured faster (1.086 vs 1.12 ms, profiles/r02p_flow_sweep.txt).
+  // The fold spreads the dx = +S column over lanes gi < K: G = S/2 >= K = 13.
+  if (S < 16 || S % 16 || S > 32 || S / 2 < FLOW_K) return false;
+  if (tuning().flow == 0) return false;
+  const int nbx_full = p.width / B;
+  if (nbx_full < 1 || p.width % 16 || p.stride % 16 || (uintptr_t)p.ref % 16 || (uintptr_t)p.cur % 16)
+    return false;
+  const int D = 2 * S + 1, K = FLOW_K, G = S / 2, chunks = (D + K - 1) / K;
+  const int rows = p.block_row_end - p.block_row_begin;
+  // The widest tile that still gives >= 6 tiles per CU (fine enough for the
+  // CUs to finish together), else the narrowest that qualifies.
+  int best_tb = 0, best_ns = 0, fine_tb = 0, fine_ns = 0;
+  for (int tb = 1; tb <= 8; tb++) {
+    if ((tb * G * chunks) % 64) continue;
+    if (tuning().plan_tb && tb != tuning().plan_tb) continue;  // tuning build
+    int pt = ((tb - 1) * B + 4 * G + B + 4 + 15) & ~15;
+    if (((pt >> 4) & 1) == 0) pt += 16;
+    const int slot = (chunks * K + B - 1) * pt + tb * B * B;
+    const int ns = min(16, (FLOW_LDS - 16 * tb * 8 - (int)sizeof(int) * 40) / slot);
+    const long tiles = (long)((nbx_full + tb - 1) / tb) * rows;
+    if (ns < 4 || tiles < 2L * cu_count()) continue;
+    if (!best_tb) {
+      best_tb = tb;
+      best_ns = ns;
+    }
+    if (tiles >= 6L * cu_count()) {
+      fine_tb = tb;
+      fine_ns = ns;
+    }
+  }
+  if (fine_tb) {
+    best_tb = fine_tb;
+    best_ns = fine_ns;
+  }
+  if (!best_tb) return false;
+  QsadGeom& q = *g;
+  q.tb = best_tb;
+  q.groups = G;
+  q.chunks = chunks;
+  q.cpp = chunks;
+  q.fold = 1;
+  q.nbx_full = nbx_full;
+  int pt = ((q.tb - 1) * B + 4 * G + B + 4 + 15) & ~15;
+  if (((pt >> 4) & 1) == 0) pt += 16;
+  q.pitch = pt;
+  q.rows_alloc = chunks * K + B - 1;
+  q.tile_bytes = q.rows_alloc * q.pitch;
+  q.wg_per_row = (nbx_full + q.tb - 1) / q.tb;
+  q.aligned = 1;
+  q.tile16 = 1;
+  q.threads = 1024;
+  q.dyn_tiles = 0;
+  q.pitch_magic = (uint32_t)(0x100000000ull / (uint64_t)q.pitch) + 1u;
+  for (uint32_t d = 0; d < (uint32_t)q.tile_bytes; d += 16)
+    if ((uint32_t)(((uint64_t)d * q.pitch_magic) >> 32) != d / (uint32_t)q.pitch) return false;
+  q.magic_groups = 0xFFFFFFFFu / (uint32_t)G + 1u;
+  for (uint32_t t = 0; t < (uint32_t)(q.tb * G * chunks); t++)
+    if ((uint32_t)(((uint64_t)t * q.magic_groups) >> 32) != t / (uint32_t)G) return false;
+  for (uint32_t nb = 2; nb <= (uint32_t)q.tb; nb++) {
+    const uint32_t mg = 0xFFFFFFFFu / nb + 1u;
+    for (uint32_t xx = 0; xx < (uint32_t)(q.tb * chunks); xx++)
+      if ((uint32_t)(((uint64_t)xx * mg) >> 32) != xx / nb) return false;
+  }
+  const int slot = q.tile_bytes + q.tb * B * B;
+  q.flow_slots = best_ns;
+  q.lds = best_ns * slot + best_ns * q.tb * 8 + (int)sizeof(int) * 40;
+  return q.lds <= 160 * 1024;
+}
+
 // Resident workgroups per CU for this kernel / block / LDS.
 static int resident_wgs(const void* fn, int threads, int lds) {
   int n = 0;
@@ -1062,11 +1387,67 @@ static bool cached_plan(const SearchArgs& p, QsadGeom* g, int* K) {
   return e.ok;
 }
 
+static bool cached_flow_plan(const SearchArgs& p, QsadGeom* g) {
+  constexpr int N = 8;
+  thread_local PlanEntry cache[N];
+  thread_local int used = 0, next = 0;
+  const int aligned = ((p.stride % 16 == 0) && ((uintptr_t)p.ref % 16 == 0) &&
+                       ((uintptr_t)p.cur % 16 == 0)) ? 3 : 0;
+  const PlanKey key{p.width, p.height, p.stride, p.blk, p.range, p.cost_kind,
+                    p.block_row_end - p.block_row_begin, aligned};
+  for (int i = 0; i < used; i++)
+    if (cache[i].key == key) {
+      *g = cache[i].g;
+      return cache[i].ok;
+    }
+  PlanEntry e;
+  e.key = key;
+  e.K = FLOW_K;
+  e.ok = plan_flow(p, &e.g);
+  cache[next] = e;
+  next = (next + 1) % N;
+  if (used < N) used++;
+  *g = e.g;
+  return e.ok;
+}
+
+static hipError_t launch_flow(const SearchArgs& p, QsadGeom g, int row0, int nrows,
+                              hipStream_t stream) {
+  if (nrows <= 0) return hipSuccess;
+  g.row0 = row0;
+  g.nrows = nrows;
+  const int ntiles = g.wg_per_row * nrows;
+  const void* fn = (const void*)me_flow_kernel<16, FLOW_K>;
+  hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, g.lds);
+  if (e != hipSuccess) return e;
+  const int nwg = ntiles < cu_count() ? ntiles : cu_count();
+  hipLaunchKernelGGL((me_flow_kernel<16, FLOW_K>), dim3((unsigned)nwg), dim3(1024), g.lds, stream, p, g);
+  return hipGetLastError();
+}
+
 static hipError_t launch_valu(const SearchArgs& p, hipStream_t stream, int* used_fast) {
   const int r0 = p.block_row_begin, r1 = p.block_row_end;
   if (r1 <= r0) return hipSuccess;
   QsadGeom g;
   int K = 0;
+  if (cached_flow_plan(p, &g)) {
+    // the flow kernel, like the item kernel, takes full-height rows and an
+    // h = B/2 bottom row; other partial bottom rows and the partial right
+    // column go to the generic kernel
+    const int nby = (p.height + p.blk - 1) / p.blk;
+    const int h_last = p.height - (nby - 1) * p.blk;
+    int rq1 = r1;
+    if (r1 == nby && h_last != p.blk && h_last != p.blk / 2) rq1 = r1 - 1;
+    hipError_t e = launch_flow(p, g, r0, rq1 - r0, stream);
+    if (e != hipSuccess) return e;
+    if (used_fast) *used_fast = 3;
+    if (rq1 < r1) {
+      e = launch_generic(p, 0, g.nbx_full, rq1, r1 - rq1, stream);
+      if (e != hipSuccess) return e;
+    }
+    if (g.nbx_full < p.nbx) return launch_generic(p, g.nbx_full, p.nbx - g.nbx_full, r0, r1 - r0, stream);
+    return hipSuccess;
+  }
   if (!cached_plan(p, &g, &K)) return launch_generic(p, 0, p.nbx, r0, r1 - r0, stream);
   // The qsad body is instantiated for full-height blocks and for h = B/2 (the
   // 1080p bottom row); any other partial bottom row goes to the generic kernel.

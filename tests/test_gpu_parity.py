@@ -283,3 +283,39 @@ def test_c_driver_reproduces_published_output(tmp_path, manifest):
     r = subprocess.run([exe, f4, f1, str(tmp_path), "8", "12", "352", "288"], capture_output=True,
                        text=True, timeout=120)
     assert "PSNR: 31.816000" in r.stdout
+
+
+def test_flow_kernel_full_frames(engine):
+    """The barrier-free SAD kernel (me_flow_kernel: 1080p-class frames, S = 32,
+    >= 2 tiles per CU) against the oracle: all-ties flat frames, noise, the
+    h = 8 bottom row, an odd block-row count, and a padded row pitch; S = 16
+    (the item kernel) beside it."""
+    import torch
+    rng = np.random.default_rng(77)
+    cases = [(1088, 1920, 32, "flat"), (1080, 1920, 32, "noise"), (1080, 1920, 16, "smooth"),
+             (1040, 2048, 32, "smooth")]
+    for h, w, span, kind in cases:
+        if kind == "flat":
+            ref = cur = np.full((h, w), 91, np.uint8)
+        elif kind == "noise":
+            ref = rng.integers(0, 256, (h, w), dtype=np.uint8)
+            cur = rng.integers(0, 256, (h, w), dtype=np.uint8)
+        else:
+            ref, cur = synth.frame_pair(w, h, 5, -6, 4)
+        mv, cost = engine.full_search(ref, cur, 16, span, "sad")
+        omv, ocost, _ = O.full_search(ref, cur, 16, span, "sad", threads=NT)
+        np.testing.assert_array_equal(mv, omv, err_msg=f"{h}x{w} S{span} {kind}")
+        np.testing.assert_array_equal(cost, ocost, err_msg=f"{h}x{w} S{span} {kind}")
+    # padded pitch (16-byte multiple) on the device API
+    ref, cur = synth.frame_pair(1920, 1080, 9, 2, -5)
+    pr, pc = np.zeros((1080, 1984), np.uint8), np.zeros((1080, 1984), np.uint8)
+    pr[:, :1920], pc[:, :1920] = ref, cur
+    n = me.num_blocks(1920, 1080, 16)
+    mvt = torch.empty((n, 2), dtype=torch.int16, device="cuda")
+    cot = torch.empty(n, dtype=torch.int32, device="cuda")
+    engine.full_search_device(torch.from_numpy(pr).cuda(), torch.from_numpy(pc).cuda(), 16, 32,
+                              "sad", mvt, cot, width=1920, height=1080, stride=1984)
+    torch.cuda.synchronize()
+    omv, ocost, _ = O.full_search(ref, cur, 16, 32, "sad", threads=NT)
+    np.testing.assert_array_equal(mvt.cpu().numpy(), omv)
+    np.testing.assert_array_equal(cot.cpu().numpy().view(np.uint32), ocost)
