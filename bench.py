@@ -352,15 +352,16 @@ def stripe_record(eng, dev, world, rank, gloo, cfg_name, cost, steps, warmup):
 
 
 def load_traffic(tag):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary of this
-    workload (tools/profile.sh), or None."""
+    """(HBM bytes per launch of the dominant kernel, per search over all its
+    kernels) from the committed rocprofv3 PMC summary of this workload
+    (tools/profile.sh), or (None, None)."""
     path = os.path.join(REPO, "profiles", "pmc_summary.json")
     try:
         with open(path) as f:
-            d = json.load(f)
-        return d.get(tag, {}).get("hbm_bytes_per_launch")
+            d = json.load(f).get(tag, {})
+        return d.get("hbm_bytes_per_launch"), d.get("hbm_bytes_per_search")
     except (OSError, ValueError):
-        return None
+        return None, None
 
 
 def main():
@@ -430,7 +431,7 @@ def main():
         absdiffs = cands_frame * blk * blk / world
     achieved = alg_bytes / (kern_ms / 1e3) / 1e9
     tag = f"{args.config}_b{blk}_s{span}_{args.cost}"
-    traffic = load_traffic(tag)
+    traffic, traffic_search = load_traffic(tag)
     line = {
         "metric": METRIC if args.config == "1080p" and args.cost == "sad" else
         f"{blk}x{blk} {args.cost.upper()} candidates/sec at {args.config} +-{span}",
@@ -455,6 +456,7 @@ def main():
         "kernel_ms": kern_ms,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_per_search": traffic_search,
                      "algorithmic_bytes_per_launch": alg_bytes,
                      "valu": {"achieved_absdiff_per_s": absdiffs / (kern_ms / 1e3),
                               "peak_absdiff_per_s": VALU_PEAK_ABSDIFF,
@@ -472,6 +474,7 @@ def main():
         hbm.pop("valu", None)
         line["roofline"] = {"bound": "mfma", "achieved": tops, "peak": I8_PEAK_TOPS,
                             "unit": "TFLOP/s", "frac": tops / I8_PEAK_TOPS, "traffic": traffic,
+                            "traffic_per_search": traffic_search,
                             "note": "useful int8 ops (2*B*B per candidate) over the whole search "
                                     "(S2 prepass + MFMA kernel); dense i8 peak",
                             "hbm": {k: hbm[k] for k in ("achieved", "peak", "unit", "frac",

@@ -68,6 +68,13 @@ d = summary[dom]
 hbm = None
 if "fetch_kib" in d and "write_kib" in d:
     hbm = 2 * d["fetch_kib"] * 1024 + d["write_kib"] * 1024
+# every kernel of one search (the SSD prepass beside its main kernel): bytes per
+# launch of each, weighted by its launches per dominant-kernel launch
+search = 0.0
+for k, v in summary.items():
+    if "fetch_kib" in v and "write_kib" in v and v.get("calls"):
+        per = v["calls"] / max(d.get("calls", 1), 1)
+        search += per * (2 * v["fetch_kib"] * 1024 + v["write_kib"] * 1024)
 bench_tag = None
 cfg = "1080p"
 cost = "sad"
@@ -85,7 +92,9 @@ except (OSError, ValueError):
     allsum = {}
 allsum[bench_tag] = {"profile_tag": tag, "dominant_kernel": dom, "kernels": summary,
                      "hbm_bytes_per_launch": hbm,
+                     "hbm_bytes_per_search": search or None,
                      "note": "hbm = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 correction, "
-                             "MI355X_MICROARCH.md §HBM); separate --pmc passes"}
+                             "MI355X_MICROARCH.md §HBM); separate --pmc passes; per_launch: the "
+                             "dominant kernel; per_search: every kernel of one search"}
 json.dump(allsum, open(path, "w"), indent=1)
 print(json.dumps(allsum[bench_tag], indent=1))

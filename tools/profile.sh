@@ -9,7 +9,7 @@
 set -o pipefail
 TAG=${1:-r01}
 shift
-ARGS=${@:---steps 20 --warmup 3 --no-cpu --no-stream}
+ARGS=${@:---steps 20 --warmup 3 --no-cpu --no-stream --no-4k}
 OUT=gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
