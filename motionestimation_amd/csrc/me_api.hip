@@ -62,6 +62,7 @@ static Tuning read_tuning() {
   env_int("ME_STREAM_COOL", 1, 64, &t.stream_cool);
   env_int("ME_STREAM_AHEAD", 1, 9, &t.stream_ahead);
   env_int("ME_FLOW", 0, 1, &t.flow);
+  env_int("ME_FLOW_SLOTS", 2, 16, &t.flow_slots);
   return t;
 }
 const Tuning& tuning() {

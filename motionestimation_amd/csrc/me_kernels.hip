@@ -902,6 +902,13 @@ __global__ __launch_bounds__(1024) void me_flow_kernel(SearchArgs p, QsadGeom g)
   int kc = 0, basec = 0, lc0c = 0, nwc = 0;  // this wave's view: item kc's first task, task count
   Item itc;
   bool have = false;
+#ifdef ME_STAMPS
+  // diagnostic build: per wave [start, first task, loop exit, spin cycles, tasks,
+  // realtime start, realtime end, hw_id] (tools/flow_stamps.py)
+  const int fw = bid * 16 + wave;
+  unsigned long long st_t0 = __builtin_amdgcn_s_memtime(), st_first = 0, st_spin = 0, st_n = 0;
+  const unsigned long long st_r0 = __builtin_amdgcn_s_memrealtime();
+#endif
   for (;;) {
     uint32_t q = 0;
     if (lane == 0) q = __hip_atomic_fetch_add(&ctl->next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -926,11 +933,22 @@ __global__ __launch_bounds__(1024) void me_flow_kernel(SearchArgs p, QsadGeom g)
     // broken invariant from hanging the GPU: the search would then be wrong,
     // which every parity test catches, instead of never finishing).
     int spins = 0;
+#ifdef ME_STAMPS
+    const unsigned long long st_w0 = __builtin_amdgcn_s_memtime();
+#endif
     while (__hip_atomic_load(&ctl->ready[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) !=
                (uint32_t)kc + 1u &&
            ++spins < (1 << 20))
       __builtin_amdgcn_s_sleep(2);
     if (spins >= (1 << 20)) break;
+#ifdef ME_STAMPS
+    {
+      const unsigned long long now = __builtin_amdgcn_s_memtime();
+      st_spin += now - st_w0;
+      if (!st_first) st_first = now;
+      st_n++;
+    }
+#endif
     const Item& it = itc;
     uint8_t* buf = smem + slot * slot_bytes;
     const uint32_t* cur_lds = reinterpret_cast<const uint32_t*>(buf + g.tile_bytes);
@@ -1030,6 +1048,15 @@ __global__ __launch_bounds__(1024) void me_flow_kernel(SearchArgs p, QsadGeom g)
       }
     }
   }
+#ifdef ME_STAMPS
+  if (lane == 0 && fw < (1 << 16)) {
+    unsigned hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    unsigned long long* o = g_stamps + 8 * fw;
+    o[0] = st_t0; o[1] = st_first; o[2] = __builtin_amdgcn_s_memtime(); o[3] = st_spin;
+    o[4] = st_n; o[5] = st_r0; o[6] = __builtin_amdgcn_s_memrealtime(); o[7] = hw;
+  }
+#endif
 }
 
 // ------------------------------------------------------------------ launch
@@ -1291,6 +1318,7 @@ bool plan_flow(const SearchArgs& p, QsadGeom* g) {
       if ((uint32_t)(((uint64_t)xx * mg) >> 32) != xx / nb) return false;
   }
   const int slot = q.tile_bytes + q.tb * B * B;
+  if (tuning().flow_slots && tuning().flow_slots < best_ns) best_ns = tuning().flow_slots;
   q.flow_slots = best_ns;
   q.lds = best_ns * slot + best_ns * q.tb * 8 + (int)sizeof(int) * 40;
   return q.lds <= 160 * 1024;

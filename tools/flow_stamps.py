@@ -1,0 +1,46 @@
+#!/usr/bin/env python3
+"""Per-wave timeline of the SAD flow kernel from the ME_STAMPS diagnostic build
+(libme_hip_stamps.so): start-up delay to the first task, time spent waiting for
+items, tasks per wave, and how the waves / CUs finish.  Diagnostic only (the
+stamps cost cycles themselves); times in shader cycles unless marked.
+usage: python3 tools/flow_stamps.py"""
+import os, sys
+import numpy as np
+import torch
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+from motionestimation_amd import _lib, synth
+_lib.LIB_PATH = os.path.join(REPO, "motionestimation_amd", "lib", "libme_hip_stamps.so")
+import ctypes
+import motionestimation_amd as me
+
+ref, cur = synth.named_pair("1080p")
+eng = me.Engine(devices=[0])
+rt, ct = torch.from_numpy(ref).cuda(), torch.from_numpy(cur).cuda()
+n = me.num_blocks(1920, 1080, 16)
+mv = torch.empty((n, 2), dtype=torch.int16, device="cuda")
+co = torch.empty(n, dtype=torch.int32, device="cuda")
+for _ in range(20):
+    eng.full_search_device(rt, ct, 16, 32, "sad", mv, co)
+torch.cuda.synchronize()
+L = _lib.lib()
+L.me_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+buf = np.zeros(8 << 16, np.uint64)
+L.me_debug_stamps(buf.ctypes.data, buf.size)
+st = buf.reshape(-1, 8)[:4096].astype(np.int64)
+st = st[st[:, 0] > 0]
+start, first, end, spin, ntask = st[:, 0], st[:, 1], st[:, 2], st[:, 3], st[:, 4]
+r0, r1 = st[:, 5], st[:, 6]
+life = end - start
+print(f"waves {len(st)}; tasks per wave: {np.bincount(ntask)}")
+print(f"start -> first task (cycles): median {np.median(first - start):.0f} p90 {np.percentile(first - start, 90):.0f} max {(first - start).max():.0f}")
+print(f"wave life: median {np.median(life):.0f}; spin share of life: median {np.median(spin / life):.3f} mean {np.mean(spin / life):.3f}")
+base = r0.min()
+print(f"realtime (us): starts {0:.2f}..{(r0.max() - base) / 100:.2f}; ends {(r1.min() - base) / 100:.2f}..{(r1.max() - base) / 100:.2f} median {(np.median(r1) - base) / 100:.2f}")
+wg = np.arange(len(st)) // 16
+cu_end = np.array([r1[wg == g].max() for g in np.unique(wg)]) - base
+cu_first_end = np.array([r1[wg == g].min() for g in np.unique(wg)]) - base
+print(f"per-CU (workgroup) end (us): min {cu_end.min()/100:.2f} median {np.median(cu_end)/100:.2f} max {cu_end.max()/100:.2f}; "
+      f"spread inside a CU (last - first wave end): median {np.median(cu_end - cu_first_end)/100:.2f}")
+clk = life / ((r1 - r0) / 100e6) / 1e9
+print(f"clock (GHz): median {np.median(clk):.3f}")
