@@ -36,11 +36,13 @@ struct Dev {
   uint32_t* mcnt = nullptr;             //   initialised on allocation, self-resetting after
   size_t merge_cap = 0;                 //   (tiles)
   // The counters, merge keys and scratch above serve one search at a time:
-  // search_ev marks the end of the last search (on search_stream); a search
-  // issued on another stream waits for it first (launch_ordered).
+  // a search issued on another stream than the previous one first waits for
+  // it (launch_ordered): a device-wide wait at the first switch, then
+  // search_ev, recorded after every search once the device has seen two streams.
   hipEvent_t search_ev = nullptr;
   hipStream_t search_stream = nullptr;
   bool searched = false;
+  bool multi_stream = false;
   // Frame-pair pipeline (me_stream.hip), kept across calls.
   std::vector<uint8_t*> slots;        // device frames, slot_bytes each
   std::vector<hipEvent_t> slot_ready; // upload of the slot's frame done (copy stream)

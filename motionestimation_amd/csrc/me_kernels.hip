@@ -1091,6 +1091,8 @@ hipError_t launch_generic(const SearchArgs& p, int bx0, int nbx_range, int row0,
 // within the LDS budget; then prefer fewer passes and smaller tiles (finer
 // work items).  256 threads per workgroup: 4 workgroups of 4 waves per CU at
 // the kernels' <= 128 VGPRs.
+static int cu_count();
+
 bool plan_fast(const SearchArgs& p, QsadGeom* g, int* k_out) {
   const int B = p.blk, S = p.range;
   if (B != 16 && B != 8) return false;
@@ -1103,7 +1105,17 @@ bool plan_fast(const SearchArgs& p, QsadGeom* g, int* k_out) {
   // Fold needs a = 0 (S % 4 == 0) and the tail words of every block aligned
   // for one ds_read of B bytes (b*B + 2S multiple of B: S % 8 == 0 for B = 16).
   const bool fold_ok = sad && S % 4 == 0 && (B == 8 || S % 8 == 0);
-  static const int Ks[] = {13, 11, 8};
+  static const int Ks[] = {13, 11, 8, 5};
+  // K = 5 (a quarter-size wave-task) only for SAD searches too small to give
+  // every SIMD two K = 13 wave-tasks (an 8-way 1080p stripe: 1.25 per SIMD, so
+  // a quarter of the SIMDs ran a second round); K >= 8 otherwise.
+  bool small = false;
+  if (sad) {
+    const int G13 = S % 4 == 0 && (B == 8 || S % 8 == 0) ? S / 2 : (2 * S + 3 + 1 + 3) / 4;
+    const double lanes = (double)(p.block_row_end - p.block_row_begin) * (p.width / B) * G13 *
+                         ((D + 12) / 13);
+    small = lanes / 64.0 < 2.0 * 4 * cu_count();
+  }
   // Tuning build override (tools/plan_sweep.py): ME_PLAN="K,tb,cpp,threads[,fold]",
   // validated in me_api.hip; 0 = free (fold: -1 = free).
   const Tuning& tu = tuning();
@@ -1122,8 +1134,22 @@ bool plan_fast(const SearchArgs& p, QsadGeom* g, int* k_out) {
     const double use_dx = sad ? (fold ? 1.0 : (double)D / (4.0 * G)) : 1.0;
     for (int K : Ks) {
       if (force[0] && K != force[0]) continue;
+      if (!force[0] && (K == 5) != small) continue;
+      if (K == 5 && (!sad || B != 16)) continue;  // instantiated for 16x16 SAD only
       if (fold && G < K) continue;
       const int chunks = (D + K - 1) / K;
+      if (K == 5 && !force[0]) {
+        // small search: one block per tile, every chunk in one pass, so each
+        // block is its own workgroup item (1,020 of them in an 8-way 1080p
+        // stripe: about one quarter-size wave-task per wave, all SIMDs busy)
+        const int pt0 = ((sad ? 4 * G + B + 4 : 2 * S + 1 + 3 + B + 4) + 15) & ~15;
+        const int pt = ((pt0 >> 4) & 1) ? pt0 : pt0 + 16;
+        const long lds = 128 + 2 * ((long)B * B + (long)(chunks * K + B - 1) * pt);
+        if (lds <= QSAD_LDS_BUDGET && best < 0) {
+          best = 1.0; bK = K; bTB = 1; bC = chunks; bF = fold; bG = G;
+        }
+        continue;
+      }
       const double kpad = (double)D / (chunks * K);
       const double tail = fold ? 0.5 * (B * CW + 16) / (K * B * CW * 4 + 340) : 0.0;
       // Waves that hold whole (block, chunk) groups (64 % G == 0 or G % 64
@@ -1366,6 +1392,7 @@ hipError_t launch_fast(const SearchArgs& p, QsadGeom g, int K, int row0, int nro
     return hipGetLastError();                                                              \
   }
   ME_FAST_CASE(COST_SAD, 16, 13) ME_FAST_CASE(COST_SAD, 16, 11) ME_FAST_CASE(COST_SAD, 16, 8)
+  ME_FAST_CASE(COST_SAD, 16, 5)
   ME_FAST_CASE(COST_SAD, 8, 13) ME_FAST_CASE(COST_SAD, 8, 11) ME_FAST_CASE(COST_SAD, 8, 8)
   ME_FAST_CASE(COST_SSD, 16, 13) ME_FAST_CASE(COST_SSD, 16, 11) ME_FAST_CASE(COST_SSD, 16, 8)
   ME_FAST_CASE(COST_SSD, 8, 13) ME_FAST_CASE(COST_SSD, 8, 11) ME_FAST_CASE(COST_SSD, 8, 8)
