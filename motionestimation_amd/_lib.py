@@ -9,7 +9,7 @@ import subprocess
 PKG = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(PKG)
 LIB_PATH = os.path.join(PKG, "lib", "libme_hip.so")
-# Diagnostic builds only (tools/ablate.sh, tools/stamps.py): another in-tree
+# Diagnostic builds only (tuning tools, tools/stamps.py): another in-tree
 # build of the same library.
 if os.environ.get("ME_HIP_LIB"):
     LIB_PATH = os.path.join(PKG, "lib", os.path.basename(os.environ["ME_HIP_LIB"]))

@@ -30,9 +30,6 @@
 #include "me_kernels.h"
 #include "me_tuning.h"
 
-#ifndef ME_ABLATE
-#define ME_ABLATE 0  // diagnostic builds only (csrc/Makefile ablate); never shipped
-#endif
 
 namespace me {
 
@@ -233,12 +230,8 @@ __device__ __forceinline__ void qsad_lane(const uint8_t* __restrict__ tile, int 
       static_for<0, K>([&](auto JJ) {
         constexpr int j = decltype(JJ)::value;
         constexpr int y = yy - j;
-#if ME_ABLATE == 2  // diagnostic: everything but the qsad issue cost
-        if constexpr (y >= 0 && y < H) acc[j] ^= (uint32_t)pr[k] ^ c[y][k];
-#else
         if constexpr (y >= 0 && y < H)
           acc[j] = __builtin_amdgcn_qsad_pk_u16_u8(pr[k], c[y][k], acc[j]);
-#endif
       });
     });
     // Pin this row's qsads inside its segment (readnone intrinsics are not
@@ -702,12 +695,6 @@ __global__ __launch_bounds__(1024) void me_fast_kernel(SearchArgs p, QsadGeom g)
       const int dxg = 4 * gi - S - it.a;  // dx of this lane's first candidate
       const bool edge = dxg < dxmin || dxg + 3 > dxmax;
       uint32_t best;
-#if ME_ABLATE == 1  // diagnostic: no epilogue
-      if (true) {
-        best = (uint32_t)(acc[0] ^ acc[K - 1]) & 0xFFFF0000u;
-        (void)edge;
-      } else
-#endif
       if (full_rows && __builtin_amdgcn_ballot_w64(edge) == 0) {
         best = lane_best<K, false>(acc, 0u, 0u, jlo, jhi);
       } else {
@@ -725,11 +712,7 @@ __global__ __launch_bounds__(1024) void me_fast_kernel(SearchArgs p, QsadGeom g)
         const bool tv = gi < K && jt >= jlo && jt <= jhi && S <= dxmax;
         best = min(best, tv ? (tsad << 16) | (uint32_t)(5 * jt + 4) : ~0u);
       }
-#if ME_ABLATE == 3  // diagnostic: no key atomics
-      if (best == 0x12345u) {
-#else
       if (best < 0xFFFF0000u) {
-#endif
         const int idx = (int)(best & 0xFFFFu), jj = idx / 5, i = idx - 5 * jj;
         const int dy = d0 + jj - S, dx = i == 4 ? S : 4 * gi + i - S - it.a;
         atomicMin(reinterpret_cast<unsigned long long*>(&keys[b]),

@@ -50,9 +50,9 @@
 #include "me_kernels.h"
 #include "me_tuning.h"
 
-#ifndef ME_MFMA_DLY
-#define ME_MFMA_DLY 1  // 1..3 (the 16-register accumulator ring holds 13 + DLY rows)
-#endif
+// Steps between a row's last MFMA and its epilogue (the 16-register accumulator
+// ring holds 13 + DLY rows); 2 and 3 measured slower (DESIGN.md, 8x8 blocks).
+constexpr int MFMA_DLY = 1;
 #ifndef ME_SSD8_KM
 #define ME_SSD8_KM 3  // 8x8 chunk length L = 16 KM: 48 rows (8K +-128: 64 rows 7.12 ms, 48 6.95-7.0, 32 8.3)
 #endif
@@ -61,9 +61,6 @@
 #endif
 #ifndef ME_SSD8_WP
 #define ME_SSD8_WP 80  // 8x8 window copy pitch: 4 x (L + 8 = 56) x 80 + S2 table (L + 1) x 256 = 30 KB at L = 48
-#endif
-#ifndef ME_MFMA_ABLATE
-#define ME_MFMA_ABLATE 0  // diagnostic bit set (csrc/Makefile mablate, tools/mablate.sh); never shipped
 #endif
 
 namespace me {
@@ -169,7 +166,6 @@ __device__ __forceinline__ void prep_tile(const SearchArgs& p, const MfmaGeom& g
     }
   }
   __syncthreads();
-#if !(ME_MFMA_ABLATE & 16)  // diagnostic: no rp stores
   if (write_rp) {
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     for (int t = tid; t < 64 * 4; t += PREP_T) {
@@ -180,7 +176,6 @@ __device__ __forceinline__ void prep_tile(const SearchArgs& p, const MfmaGeom& g
                                     reinterpret_cast<u32x4*>(g.rp + (ptrdiff_t)rr * g.pitch + x0 + xs));
     }
   }
-#endif
   // Horizontal sums, 4 outputs per task: consecutive lanes store consecutive
   // 16-byte groups (a wave's store covers 1 KB of whole lines; 16-output tasks
   // wrote 16 bytes per 64 and measured half the write bandwidth).
@@ -206,16 +201,8 @@ __device__ __forceinline__ void prep_tile(const SearchArgs& p, const MfmaGeom& g
         o[j] = (yok && x0 + xs + j <= W - BW) ? sacc : 0;
         if (j < 3) sacc += v[j + BW] - v[j];
       }
-#if ME_MFMA_ABLATE & 8  // diagnostic: no s2 stores
-      if (o[0] == 0x7FFFFFF0 && o[3] == 3) plane[0] = o[1];
-      continue;
-#endif
       // non-temporal: the planes are read by the next kernel, not this one
-#if ME_MFMA_ABLATE & 4096  // diagnostic: plain stores
-      *reinterpret_cast<i32x4*>(plane + (ptrdiff_t)yy * g.pitch + x0 + xs) = o;
-#else
       __builtin_nontemporal_store(o, reinterpret_cast<i32x4*>(plane + (ptrdiff_t)yy * g.pitch + x0 + xs));
-#endif
     }
   }
 }
@@ -259,11 +246,7 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, uint8_t* lds_ds
   }
 }
 
-#if ME_MFMA_ABLATE & 64  // diagnostic: no MFMA (one VALU op instead)
-#define MFMA16(A, B, C, x, y, z) ((C) + ((A) ^ (B)))
-#else
 #define MFMA16 __builtin_amdgcn_mfma_i32_16x16x64_i8
-#endif
 
 __device__ __forceinline__ uint32_t sad_u32(uint32_t a_sgpr, uint32_t b, uint32_t c) {
   uint32_t d;
@@ -294,7 +277,7 @@ __global__ __launch_bounds__(256 * NGX)
 __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd16_kernel(SearchArgs p, MfmaGeom g) {
   // NGX 64-position groups per workgroup (4 waves each)
   constexpr int WP = 64 * NGX + 32;  // bytes per copy row
-  constexpr int DLY = ME_MFMA_DLY;      // steps between a row's last MFMA and its epilogue
+  constexpr int DLY = MFMA_DLY;         // steps between a row's last MFMA and its epilogue
   constexpr int P0 = 12 + DLY;         // prologue steps (= epilogue lag)
   constexpr int L = P0 + 16 * KM;      // candidate rows per chunk
   constexpr int CROWS = L + 15;
@@ -450,13 +433,8 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd16_kernel(SearchArgs p, 
     const int c = cc[4 * h + r];
     initv[r] = ok ? (c >> 1) : (c >> 1) + (1 << 23);
   }
-#if ME_MFMA_ABLATE & 128  // diagnostic: every lane group reads the same row (no bank conflicts)
-  const uint32_t lds_lane = (uint32_t)(uintptr_t)(
-      (__attribute__((address_space(3))) uint8_t*)smem) + (uint32_t)(sig * COPY + ccol);
-#else
   const uint32_t lds_lane = (uint32_t)(uintptr_t)(
       (__attribute__((address_space(3))) uint8_t*)smem) + (uint32_t)(sig * COPY + h * WP + ccol);
-#endif
   const uint32_t s2t_lane = (uint32_t)(uintptr_t)(
       (__attribute__((address_space(3))) uint8_t*)s2t) + (uint32_t)(64 * (gx - gx0) + 4 * n + s) * 4u;
   const bool active = gx < ngx;
@@ -466,9 +444,7 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd16_kernel(SearchArgs p, 
     if (ch > 0) {
       __syncthreads();  // every wave done with the previous chunk's copies
       if (ch == 1) MS_STAMP(2, __builtin_amdgcn_s_memtime());
-#if !(ME_MFMA_ABLATE & 4)  // diagnostic: stage the first chunk only
       stage(y0);
-#endif
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       shift_copies();
@@ -491,18 +467,11 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd16_kernel(SearchArgs p, 
         lp += 4 * WP;
         asm volatile("" : "+v"(lp));
       }
-#if ME_MFMA_ABLATE & 32  // diagnostic: no fragment loads in the loop
-      dst = a[0] ^ (int)lp;
-#else
       lds_u32* w = reinterpret_cast<lds_u32*>((uintptr_t)lp + (row & 3) * WP);
       dst[0] = (int)w[0]; dst[1] = (int)w[1]; dst[2] = (int)w[2]; dst[3] = (int)w[3];
-#endif
     };
     uint32_t sp = s2t_lane;  // S2 table row 16k of the main loop
     auto s2load = [&](int yrel_static_off, int yrel) -> int {
-#if ME_MFMA_ABLATE & 1  // diagnostic: no S2 loads
-      return yrel;
-#else
       if constexpr (decltype(HBC)::value) {
         // the lanes' S2 planes differ (s2 / s2h): straight from global memory
         (void)yrel_static_off;
@@ -512,13 +481,8 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd16_kernel(SearchArgs p, 
         (void)yrel;
         return *reinterpret_cast<lds_i32*>((uintptr_t)(sp + (uint32_t)yrel_static_off * RB));
       }
-#endif
     };
     auto epi = [&](int yrel, const v4i& av, int s2v) {
-#if ME_MFMA_ABLATE & 2  // diagnostic: epilogue reduced to one min per step
-      best[0] = min(best[0], (uint32_t)(av[0] ^ av[1] ^ av[2] ^ av[3] ^ s2v));
-      return;
-#endif
       const uint32_t P = lshl6_add((uint32_t)s2v, (uint32_t)(64 + yrel));
       const uint32_t Wd = sad_u32((uint32_t)(2 * (y0 + yrel)), sumLH, Cv);
       const uint32_t Pf = (Wd & 0x80000000u) | P;
@@ -730,9 +694,6 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd8_kernel(SearchArgs p, M
       return (uint32_t)(base + rho * g.pitch + k);
     });
     const int sbase = ((y0 - g.ya0) * g.pitch + xa + 64 * gx) * 4;
-#if ME_MFMA_ABLATE & 1  // diagnostic: no S2 table staging
-    if (opaque(0))
-#endif
     dma16(rs2, s2t, L * RB, [&](int d) {
       const int rho = d / RB, k = d - rho * RB;
       return (uint32_t)(sbase + rho * g.pitch * 4 + k);
@@ -819,11 +780,7 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd8_kernel(SearchArgs p, M
 
   for (int ch = 0; ch < nch; ch++) {
     const int y0 = ya + ch * L;
-#if ME_MFMA_ABLATE & 4  // diagnostic: only the first chunk staged
-    if (opaque(0)) {
-#else
     if (ch > 0) {
-#endif
       __syncthreads();
       stage(y0);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -855,13 +812,8 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd8_kernel(SearchArgs p, M
         const uint32_t Wd = sad_u32((uint32_t)(2 * (y0 + yrel)), sumLH, Cv);
         Pf = (Wd & 0x80000000u) | Pf;
       }
-#if ME_MFMA_ABLATE & 2  // diagnostic: epilogue cut to the accumulator
-      for (int r = 0; r < 4; r++) k[r] = (uint32_t)av[r];
-      (void)Pf;
-#else
 #pragma unroll
       for (int r = 0; r < 4; r++) k[r] = ((uint32_t)av[r] << 7) + Pf;
-#endif
     };
     auto body = [&](auto MASKED) {
       v2i rw[3];  // window rows t+2h (older), t+2h+1, and the prefetched t+2h+2
@@ -1155,12 +1107,8 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_bm16_kernel(SearchArgs p, M
       auto tile = [&](int i, auto DA, auto DB, auto MA, auto MB) {
         constexpr bool da = decltype(DA)::value, db = decltype(DB)::value;
         constexpr int ma = decltype(MA)::value, mb = decltype(MB)::value;
-#if ME_MFMA_ABLATE & 256  // diagnostic: no S2 loads
-        const v4i s2c = {n, h, s, i};
-#else
         const v4i s2c = __builtin_bit_cast(
             v4i, __builtin_amdgcn_raw_buffer_load_b128(rs2, s2v, srow + 64 * i, 0));
-#endif
         // one base per tile, fragment rows at immediate offsets
         const uint32_t lrow = (uint32_t)opaque((int)(lrow0 + (uint32_t)(16 * i)));
         v4i accA = ma == 1 ? mF : ma == 2 ? mL : zero4;
@@ -1168,12 +1116,7 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_bm16_kernel(SearchArgs p, M
         // Fragments in pairs, the next pair in flight during this pair's MFMAs
         // (four fragments live: the A fragments hold 64 VGPRs).
         auto ld = [&](int q) {
-#if ME_MFMA_ABLATE & 2048  // diagnostic: no fragment loads
-          const v4i t = {(int)lrow, q, 0, 0};
-          return t;
-#else
           return *reinterpret_cast<lds_v4i*>((uintptr_t)(lrow + (uint32_t)(2 * q * BM_LP)));
-#endif
         };
         v4i f0 = ld(0), f1 = ld(1);
 #pragma unroll
@@ -1208,10 +1151,6 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_bm16_kernel(SearchArgs p, M
                 acc[r] += (int)(__builtin_amdgcn_ubfe(mb4, (uint32_t)(4 * e + r), 1u) << 24);
             }
           }
-#if ME_MFMA_ABLATE & 512  // diagnostic: epilogue cut to one min
-          best = min(best, (uint32_t)(acc[0] ^ acc[1] ^ acc[2] ^ acc[3]) ^ P[0]);
-          return;
-#endif
           uint32_t k[4];
 #pragma unroll
           for (int r = 0; r < 4; r++) k[r] = ((uint32_t)acc[r] << 7) + P[r];
@@ -1363,11 +1302,11 @@ bool plan_mfma_ssd(const SearchArgs& p, MfmaGeom* g) {
   const int force_km = tuning().mfma_km;  // ME_MFMA_KM=2|3: tuning build override
   for (int km = 2; km <= 3; km++) {  // km = 1 spills (its lone main-loop pass gets peeled)
     if (force_km && km != force_km) continue;
-    const int L = 12 + ME_MFMA_DLY + 16 * km, ch = (ny + L - 1) / L;
-    const int cost = ch * (L + 12 + ME_MFMA_DLY);
+    const int L = 12 + MFMA_DLY + 16 * km, ch = (ny + L - 1) / L;
+    const int cost = ch * (L + 12 + MFMA_DLY);
     if (cost < best) { best = cost; g->km = km; }
   }
-  const int L = 12 + ME_MFMA_DLY + 16 * g->km;
+  const int L = 12 + MFMA_DLY + 16 * g->km;
   // groups per workgroup: two when the tile needs an even number of groups
   // (whole tiles at 1080p +-32: no merge), else one (4K +-64: 3 workgroups)
   g->ngxw = ngx % 2 == 0 ? 2 : 1;
