@@ -44,3 +44,40 @@ print(f"per-CU (workgroup) end (us): min {cu_end.min()/100:.2f} median {np.media
       f"spread inside a CU (last - first wave end): median {np.median(cu_end - cu_first_end)/100:.2f}")
 clk = life / ((r1 - r0) / 100e6) / 1e9
 print(f"clock (GHz): median {np.median(clk):.3f}")
+
+# Where the SIMD-cycles go: hw_id (gfx9 HW_REG_HW_ID) bits 5:4 = SIMD; workgroup
+# b runs on XCD b % 8 (round-robin dispatch).  Per SIMD: idle before its first
+# task (from the kernel's first wave start) and after its last wave ends (to
+# the kernel's last wave end), in us of realtime.
+hw = st[:, 7]
+simd = (hw >> 4) & 3
+kend = r1.max()
+first_rt = r0 + (first - start) / np.maximum(clk, 1e-3) / 10.0  # cycles -> 10 ns ticks
+lead, tail, cu_tail, simd_spread = [], [], [], []
+for g in np.unique(wg):
+    sel = wg == g
+    cu_e = r1[sel].max()
+    cu_tail.append((kend - cu_e) / 100)
+    ends = []
+    for s in range(4):
+        ss = sel & (simd == s)
+        if not ss.any():
+            continue
+        lead.append((first_rt[ss].min() - base) / 100)
+        e = r1[ss].max()
+        ends.append(e)
+        tail.append((kend - e) / 100)
+    simd_spread.append((max(ends) - min(ends)) / 100)
+lead, tail = np.array(lead), np.array(tail)
+span = (kend - base) / 100
+print(f"span {span:.2f} us; per SIMD: lead-in (first task) mean {lead.mean():.2f} us, "
+      f"tail (idle after its last wave) mean {tail.mean():.2f} us "
+      f"= {100 * (lead.mean() + tail.mean()) / span:.1f} % of the span")
+print(f"  CU tail (kernel end - CU end) mean {np.mean(cu_tail):.2f} us; SIMD end spread inside a CU "
+      f"median {np.median(simd_spread):.2f} p90 {np.percentile(simd_spread, 90):.2f} us")
+xcd = np.unique(wg) % 8
+cu_e = np.array([r1[wg == g].max() for g in np.unique(wg)]) - base
+for x in range(8):
+    sx = np.isin(wg, np.unique(wg)[xcd == x])
+    print(f"  XCD {x}: clock {np.median(clk[sx]):.3f} GHz, CU end median {np.median(cu_e[xcd == x]) / 100:.2f} "
+          f"max {cu_e[xcd == x].max() / 100:.2f} us, tasks {ntask[sx].sum()}")
