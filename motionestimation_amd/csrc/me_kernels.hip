@@ -1117,8 +1117,9 @@ bool plan_fast(const SearchArgs& p, QsadGeom* g, int* k_out) {
     const double use_dx = sad ? (fold ? 1.0 : (double)D / (4.0 * G)) : 1.0;
     for (int K : Ks) {
       if (force[0] && K != force[0]) continue;
-      if (!force[0] && (K == 5) != small) continue;
-      if (K == 5 && (!sad || B != 16)) continue;  // instantiated for 16x16 SAD only
+      // (K = 5 is instantiated for 16x16 SAD only: other small searches keep K >= 8)
+      if (K == 5 && (!sad || B != 16)) continue;
+      if (!force[0] && (K == 5) != (small && B == 16)) continue;
       if (fold && G < K) continue;
       const int chunks = (D + K - 1) / K;
       if (K == 5 && !force[0]) {
@@ -1158,17 +1159,21 @@ bool plan_fast(const SearchArgs& p, QsadGeom* g, int* k_out) {
           for (int c0 = 0; c0 < chunks; c0 += cpp) passes++;
           const long items = (long)((g->nbx_full + tb - 1) / tb) * rows * passes;
           // Cost of an item in wave-tasks: its waves (a partly filled wave
-          // costs a whole one) + ~0.45 for staging, barrier and output
-          // (fitted on tools/plan_sweep.py runs).  With few items per
-          // workgroup (< 8 of 1024) a partial last round of the workgroup
-          // is not amortised: count whole rounds of `thr` lanes instead.
+          // costs a whole one), for SAD half of the wave slots its last round of
+          // `thr` lanes leaves idle (the CU's other workgroups take up the
+          // rest: 4K +-64, 68 block rows, tb 5 = 10 waves in rounds of 4:
+          // 0.637 ms against tb 8's 0.570, profiles/r02aa_plan_sweep_4k_68rows.jsonl),
+          // + ~0.45 for staging, barrier and output (fitted on
+          // tools/plan_sweep.py runs).  With few items per workgroup (< 8 of
+          // 1024) a partial last round is not amortised at all: whole rounds.
           const bool many = items >= 8L * 1024;
           double cost = 0, useful = 0;
           for (int c0 = 0; c0 < chunks; c0 += cpp) {
             const int t = tb * G * (chunks - c0 < cpp ? chunks - c0 : cpp);
             const int rounds = (t + thr - 1) / thr;
+            const int waves = (t + 63) / 64, idle = rounds * (thr / 64) - waves;
             // few items: every extra round lengthens the kernel's tail too
-            cost += (many ? (t + 63) / 64 : rounds * (thr / 64) + 0.5 * (rounds - 1)) + 0.45;
+            cost += (many ? waves + (sad ? 0.5 * idle : 0.0) : rounds * (thr / 64) + 0.5 * (rounds - 1)) + 0.45;
             useful += t / 64.0;
           }
           // Workgroups take whole tiles (every pass of a tile runs on the
