@@ -184,12 +184,16 @@ __device__ __forceinline__ void pin_rows32(uint32_t (&acc)[K]) {
   }
 }
 
-template <int B, int K, int H>
+// PC > 0: the pitch is that compile-time constant, and the rows of a group of
+// RG share one base address (the row offset goes into the ds_read2 offset
+// fields, <= 1020 bytes): one address add per group instead of per row.
+template <int B, int K, int H, int PC = 0>
 __device__ __forceinline__ void qsad_lane(const uint8_t* __restrict__ tile, int pitch,
                                           uint32_t buf_off, int lrow, int w0,
                                           const uint32_t (&c)[B][B / 4], uint64_t (&acc)[K]) {
   constexpr int CW = B / 4;
   constexpr int NR = K + H - 1;
+  constexpr int RG = PC > 0 ? ((1020 - 4 * CW) / PC + 1 < 8 ? (1020 - 4 * CW) / PC + 1 : 8) : 1;
   // Operand pair k = ref words (w0 + k, w0 + k + 1) of the current row: one
   // ds_read2_b32 straight into an aligned VGPR pair.  Pairs 0, 2 come from
   // byte offset oe = 4*w0, pairs 1, 3 from oo = oe + 4; both advance through
@@ -206,24 +210,34 @@ __device__ __forceinline__ void qsad_lane(const uint8_t* __restrict__ tile, int 
   // LDS addresses as plain integers (address space 3, base folded into oe/oo
   // once) so no per-row add of the dynamic-LDS symbol survives.
   typedef __attribute__((address_space(3))) const uint32_t lds_u32;
-  auto load = [&](uint64_t (&dst)[CW]) {
+  auto load = [&](uint64_t (&dst)[CW], uint32_t ro) {
 #pragma unroll
     for (int k = 0; k < CW; k++) {
-      lds_u32* w = reinterpret_cast<lds_u32*>((uintptr_t)((k & 1) ? oo : oe)) + 2 * (k >> 1);
+      lds_u32* w = reinterpret_cast<lds_u32*>((uintptr_t)(((k & 1) ? oo : oe) + ro)) + 2 * (k >> 1);
       dst[k] = ((uint64_t)w[1] << 32) | w[0];
     }
   };
   uint64_t pr[CW], nx[CW];
-  load(pr);
+  load(pr, 0);
   static_for<0, NR>([&](auto YY) {
     constexpr int yy = decltype(YY)::value;
     // one segment per window row: next row's loads, then this row's qsads.
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (yy + 1 < NR) {
-      oe += pitch;
-      oo += pitch;
-      asm volatile("" : "+v"(oe), "+v"(oo));
-      load(nx);
+      if constexpr (PC > 0) {
+        constexpr int nr = yy + 1;
+        if constexpr (nr % RG == 0) {
+          oe += RG * PC;
+          oo += RG * PC;
+          asm volatile("" : "+v"(oe), "+v"(oo));
+        }
+        load(nx, (uint32_t)((nr % RG) * PC));
+      } else {
+        oe += pitch;
+        oo += pitch;
+        asm volatile("" : "+v"(oe), "+v"(oo));
+        load(nx, 0);
+      }
     }
     static_for<0, CW>([&](auto KK) {
       constexpr int k = decltype(KK)::value;
@@ -835,7 +849,7 @@ __device__ __forceinline__ int flow_tasks(const SearchArgs& p, const QsadGeom& g
   return ((lc1 - lc0) * it.nb * g.groups + 63) >> 6;
 }
 
-template <int B, int K>
+template <int B, int K, int PC>
 __global__ __launch_bounds__(1024) void me_flow_kernel(SearchArgs p, QsadGeom g) {
   static_assert(B == 16, "cur-block DMA layout of stage_item_wave");
   constexpr int CW = B / 4;
@@ -874,6 +888,12 @@ __global__ __launch_bounds__(1024) void me_flow_kernel(SearchArgs p, QsadGeom g)
   __syncthreads();
   // wave w < NB stages item w and publishes it
   if (wave < NB && wave < nitems) {
+    // Staggered start (wave w waits w x 640 cycles): item 0's DMA gets the
+    // CU's memory pipeline first and lands early instead of every item
+    // landing together at the end of one burst (1080p, same box:
+    // 78.4 -> 78.0 us; with the compile-time pitch 79.0 -> 77.3,
+    // profiles/r02ae_ab_flow_start.txt).
+    for (int i = 0; i < wave; i++) __builtin_amdgcn_s_sleep(10);
     stage_item_wave<B>(p, g, item_of<B, K>(p, g, tile_of(wave), 0), smem + wave * slot_bytes, rref,
                        rcur);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -974,10 +994,10 @@ __global__ __launch_bounds__(1024) void me_flow_kernel(SearchArgs p, QsadGeom g)
     const uint32_t toff = tile_off + (uint32_t)((lc * K + jt) * g.pitch + b * B + 2 * S);
     uint32_t tsad = 0;
     if (it.h == B) {
-      qsad_lane<B, K, B>(smem, g.pitch, tile_off, lc * K, w0, c, acc);
+      qsad_lane<B, K, B, PC>(smem, g.pitch, tile_off, lc * K, w0, c, acc);
       if (g.fold) tsad = tail_sad<B, B>(smem, g.pitch, toff, c);
     } else {
-      qsad_lane<B, K, B / 2>(smem, g.pitch, tile_off, lc * K, w0, c, acc);
+      qsad_lane<B, K, B / 2, PC>(smem, g.pitch, tile_off, lc * K, w0, c, acc);
       if (g.fold) tsad = tail_sad<B, B / 2>(smem, g.pitch, toff, c);
     }
     const int dxg = 4 * gi - S - it.a;
@@ -1460,11 +1480,17 @@ static hipError_t launch_flow(const SearchArgs& p, QsadGeom g, int row0, int nro
   g.row0 = row0;
   g.nrows = nrows;
   const int ntiles = g.wg_per_row * nrows;
-  const void* fn = (const void*)me_flow_kernel<16, FLOW_K>;
+  // 144: the pitch of the 4-block tiles 1080p +-32 gets (row addresses in
+  // the ds_read2 offsets); any other pitch takes the runtime-pitch body
+  const void* fn = g.pitch == 144 ? (const void*)me_flow_kernel<16, FLOW_K, 144>
+                                  : (const void*)me_flow_kernel<16, FLOW_K, 0>;
   hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, g.lds);
   if (e != hipSuccess) return e;
   const int nwg = ntiles < cu_count() ? ntiles : cu_count();
-  hipLaunchKernelGGL((me_flow_kernel<16, FLOW_K>), dim3((unsigned)nwg), dim3(1024), g.lds, stream, p, g);
+  if (g.pitch == 144)
+    hipLaunchKernelGGL((me_flow_kernel<16, FLOW_K, 144>), dim3((unsigned)nwg), dim3(1024), g.lds, stream, p, g);
+  else
+    hipLaunchKernelGGL((me_flow_kernel<16, FLOW_K, 0>), dim3((unsigned)nwg), dim3(1024), g.lds, stream, p, g);
   return hipGetLastError();
 }
 
