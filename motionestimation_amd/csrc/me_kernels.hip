@@ -537,7 +537,7 @@ __device__ __forceinline__ void stage_item(const SearchArgs& p, const QsadGeom& 
 // walk one contiguous band of tiles, so each XCD's L2 holds one band of rows.
 // Item k of a workgroup = (its k / passes-th tile, pass k % passes); while
 // item k is computed from LDS buffer k & 1, item k + 1 streams into the other.
-template <int COST, int B, int K>
+template <int COST, int B, int K, int PC = 0>
 __global__ __launch_bounds__(1024) void me_fast_kernel(SearchArgs p, QsadGeom g) {
   constexpr int CW = B / 4;
   extern __shared__ __align__(16) uint8_t smem[];
@@ -698,10 +698,10 @@ __global__ __launch_bounds__(1024) void me_fast_kernel(SearchArgs p, QsadGeom g)
       const uint32_t toff = tile_off + (uint32_t)((lc * K + jt) * g.pitch + b * B + 2 * S);
       uint32_t tsad = 0;
       if (it.h == B) {
-        qsad_lane<B, K, B>(smem, g.pitch, tile_off, lc * K, w0, c, acc);
+        qsad_lane<B, K, B, PC>(smem, g.pitch, tile_off, lc * K, w0, c, acc);
         if (g.fold) tsad = tail_sad<B, B>(smem, g.pitch, toff, c);
       } else {
-        qsad_lane<B, K, B / 2>(smem, g.pitch, tile_off, lc * K, w0, c, acc);
+        qsad_lane<B, K, B / 2, PC>(smem, g.pitch, tile_off, lc * K, w0, c, acc);
         if (g.fold) tsad = tail_sad<B, B / 2>(smem, g.pitch, toff, c);
       }
       // Waves with no frame-edge candidate (most of them) take the unmasked
@@ -1385,9 +1385,11 @@ hipError_t launch_fast(const SearchArgs& p, QsadGeom g, int K, int row0, int nro
   g.nrows = nrows;
   const int ntiles = g.wg_per_row * nrows;
   dim3 block((unsigned)g.threads);
-#define ME_FAST_CASE(CC, BB, KK)                                                           \
-  if (p.cost_kind == CC && p.blk == BB && K == KK) {                                       \
-    const void* fn = (const void*)me_fast_kernel<CC, BB, KK>;                              \
+// PP > 0: the instance with that compile-time tile pitch (row addresses in the
+// ds_read2 offset fields), taken when the plan has exactly that pitch.
+#define ME_FAST_CASE_P(CC, BB, KK, PP)                                                     \
+  if (p.cost_kind == CC && p.blk == BB && K == KK && (PP == 0 || g.pitch == PP)) {         \
+    const void* fn = (const void*)me_fast_kernel<CC, BB, KK, PP>;                         \
     if (g.lds > 64 * 1024) {                                                               \
       hipError_t e_ = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, g.lds); \
       if (e_ != hipSuccess) return e_;                                                     \
@@ -1396,15 +1398,21 @@ hipError_t launch_fast(const SearchArgs& p, QsadGeom g, int K, int row0, int nro
     if (res_lds != g.lds) { res_n = resident_wgs(fn, g.threads, g.lds); res_lds = g.lds; } \
     const int res = res_n;                                                                 \
     const int nwg = ntiles < res * cu_count() ? ntiles : res * cu_count();                 \
-    hipLaunchKernelGGL((me_fast_kernel<CC, BB, KK>), dim3((unsigned)nwg), block, g.lds, stream, p, g); \
+    hipLaunchKernelGGL((me_fast_kernel<CC, BB, KK, PP>), dim3((unsigned)nwg), block, g.lds, stream, p, g); \
     return hipGetLastError();                                                              \
   }
+#define ME_FAST_CASE(CC, BB, KK) ME_FAST_CASE_P(CC, BB, KK, 0)
+  // the plans' pitches of 4K +-64 (tb 8: 272; 1.098 -> 1.085 ms) and 8K 8x8
+  // +-128 (tb 8: 336; 18.59 -> 18.19 ms); the 1080p stripes' pitches (144,
+  // 112) measured no better (profiles/r02ah_ab_item_pitch.txt)
+  ME_FAST_CASE_P(COST_SAD, 16, 13, 272) ME_FAST_CASE_P(COST_SAD, 8, 13, 336)
   ME_FAST_CASE(COST_SAD, 16, 13) ME_FAST_CASE(COST_SAD, 16, 11) ME_FAST_CASE(COST_SAD, 16, 8)
   ME_FAST_CASE(COST_SAD, 16, 5)
   ME_FAST_CASE(COST_SAD, 8, 13) ME_FAST_CASE(COST_SAD, 8, 11) ME_FAST_CASE(COST_SAD, 8, 8)
   ME_FAST_CASE(COST_SSD, 16, 13) ME_FAST_CASE(COST_SSD, 16, 11) ME_FAST_CASE(COST_SSD, 16, 8)
   ME_FAST_CASE(COST_SSD, 8, 13) ME_FAST_CASE(COST_SSD, 8, 11) ME_FAST_CASE(COST_SSD, 8, 8)
 #undef ME_FAST_CASE
+#undef ME_FAST_CASE_P
   return hipErrorInvalidValue;
 }
 
