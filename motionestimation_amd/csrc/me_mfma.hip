@@ -157,6 +157,7 @@ __device__ __forceinline__ void prep_tile(const SearchArgs& p, const MfmaGeom& g
       vs[(y0 + j) * VS_P + c] = s;
       if (j < 15) s += sq127(v[j + BH]) - sq127(v[j]);
     }
+    PS_STAMP(1);
     if (write_rp && c < 64) {  // rp bytes via LDS: stored as whole 16-byte groups below
 #pragma unroll
       for (int j = 0; j < 16; j++) {
@@ -166,6 +167,7 @@ __device__ __forceinline__ void prep_tile(const SearchArgs& p, const MfmaGeom& g
     }
   }
   __syncthreads();
+  PS_STAMP(2);
   if (write_rp) {
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     for (int t = tid; t < 64 * 4; t += PREP_T) {

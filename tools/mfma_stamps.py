@@ -68,6 +68,9 @@ ps = pb.reshape(-1, 6)
 full = ps[(ps[:, 3] > 0)].astype(np.float64)
 print(f"prepass: {len(full)} main workgroups; lifetime cycles median {np.median(full[:, 3] - full[:, 0]):.0f}, "
       f"max {np.max(full[:, 3] - full[:, 0]):.0f}")
+for nm, a0, a1 in (("loads + vertical sums (thread 0)", 0, 1), ("to the barrier", 1, 2), ("stores", 2, 3)):
+    d = full[:, a1] - full[:, a0]
+    print(f"  prepass {nm}: median {np.median(d):.0f} p90 {np.percentile(d, 90):.0f} cycles")
 ra, rb = full[:, 4] - full[:, 4].min(), full[:, 5] - full[:, 4].min()
 print(f"prepass realtime us: starts min {ra.min()/100:.2f} median {np.median(ra)/100:.2f} max {ra.max()/100:.2f}; "
       f"ends max {rb.max()/100:.2f}")
