@@ -617,6 +617,7 @@ __global__ __launch_bounds__(1024) void me_fast_kernel(SearchArgs p, QsadGeom g)
     uint8_t* buf = smem + (k & 1) * buf_bytes;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();  // item k staged by every wave; item k-1 fully consumed
+    if (k == 0) ME_STAMP(2, __builtin_amdgcn_s_memtime());  // first item staged
     if (dyn && pass == 0 && tid == 0) {  // starting tile ti: pull tile ti + 2
       const int prev = tq[(ti + 1) & 3];
       tq[(ti + 2) & 3] = prev >= 0 ? pull() : -1;
@@ -761,7 +762,6 @@ __global__ __launch_bounds__(1024) void me_fast_kernel(SearchArgs p, QsadGeom g)
     }
   }
   ME_STAMP(1, (unsigned long long)nitems);
-  ME_STAMP(2, __builtin_amdgcn_s_memtime());
   if (dyn && tid == 0) {
     // The last workgroup out re-zeroes the counters for the next launch on
     // this stream (every other workgroup's final pull precedes its arrival).
@@ -1108,6 +1108,12 @@ bool plan_fast(const SearchArgs& p, QsadGeom* g, int* k_out) {
   // Fold needs a = 0 (S % 4 == 0) and the tail words of every block aligned
   // for one ds_read of B bytes (b*B + 2S multiple of B: S % 8 == 0 for B = 16).
   const bool fold_ok = sad && S % 4 == 0 && (B == 8 || S % 8 == 0);
+  // SAD rows carry an alignment word for a = (tlx - S) mod 4 <= 3; with S % 4
+  // == 0 (tlx a multiple of B) a = 0 and the lanes read exactly 4G + B bytes
+  // past the block's first tile column: no word (1080p tb = 3 rows 112 instead
+  // of 144 bytes; the 2- and 4-way stripe times moved within box-to-box
+  // noise, profiles/r02al_stripe_sweeps.jsonl)
+  const int aw = S % 4 == 0 ? 0 : 4;
   static const int Ks[] = {13, 11, 8, 5};
   // K = 5 (a quarter-size wave-task) only for SAD searches too small to give
   // every SIMD two K = 13 wave-tasks (an 8-way 1080p stripe: 1.25 per SIMD, so
@@ -1145,8 +1151,11 @@ bool plan_fast(const SearchArgs& p, QsadGeom* g, int* k_out) {
       if (K == 5 && !force[0]) {
         // small search: one block per tile, every chunk in one pass, so each
         // block is its own workgroup item (1,020 of them in an 8-way 1080p
-        // stripe: about one quarter-size wave-task per wave, all SIMDs busy)
-        const int pt0 = ((sad ? 4 * G + B + 4 : 2 * S + 1 + 3 + B + 4) + 15) & ~15;
+        // stripe: about one quarter-size wave-task per wave, all SIMDs busy).
+        // No fold (17 groups): the fold's narrower rows measured slower here
+        // (9-row stripe 20.2 vs 19.65 us, CIF +-16 12.4 vs 11.05 us,
+        // profiles/r02am_small_plan_fold.txt).
+        const int pt0 = ((sad ? 4 * G + B + aw : 2 * S + 1 + 3 + B + 4) + 15) & ~15;
         const int pt = ((pt0 >> 4) & 1) ? pt0 : pt0 + 16;
         const long lds = 128 + 2 * ((long)B * B + (long)(chunks * K + B - 1) * pt);
         if (lds <= QSAD_LDS_BUDGET && best < 0) {
@@ -1168,7 +1177,7 @@ bool plan_fast(const SearchArgs& p, QsadGeom* g, int* k_out) {
         // stripe of an 8-way split: 0.228 vs 0.188 ms; profiles/r02h_dyn.jsonl).
         if (tb == 1 && !force[1] && g->nbx_full >= 2) continue;
         // bytes the lanes touch per row (+ a <= 3, + alignment word)
-        const int width = (tb - 1) * B + (sad ? 4 * G + B + 4 : 2 * S + 1 + 3 + B + 4);
+        const int width = (tb - 1) * B + (sad ? 4 * G + B + aw : 2 * S + 1 + 3 + B + 4);
         int pt = (width + 15) & ~15;
         if (((pt >> 4) & 1) == 0) pt += 16;
         for (int cpp = chunks; cpp >= 1; cpp--) {
@@ -1239,7 +1248,7 @@ bool plan_fast(const SearchArgs& p, QsadGeom* g, int* k_out) {
   g->chunks = (D + bK - 1) / bK;
   // recompute the pitch of the chosen tb
   {
-    const int width = (g->tb - 1) * B + (sad ? 4 * g->groups + B + 4 : 2 * S + 1 + 3 + B + 4);
+    const int width = (g->tb - 1) * B + (sad ? 4 * g->groups + B + aw : 2 * S + 1 + 3 + B + 4);
     int pt = (width + 15) & ~15;
     if (((pt >> 4) & 1) == 0) pt += 16;
     g->pitch = pt;

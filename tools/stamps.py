@@ -2,7 +2,7 @@
 """Per-workgroup timeline of the qsad kernel from the ME_STAMPS diagnostic
 build (libme_hip_stamps.so): staging / compute / epilogue shares, per-CU
 concurrency and the tail.  Diagnostic only: its absolute time is not quoted.
-usage: python3 tools/stamps.py [1080p|4k|8k]"""
+usage: python3 tools/stamps.py [1080p|4k|8k] [r0:r1 (one stripe's block rows)]"""
 import ctypes, os, sys
 import numpy as np
 import torch
@@ -21,8 +21,13 @@ rt, ct = torch.from_numpy(ref).cuda(), torch.from_numpy(cur).cuda()
 n = me.num_blocks(w, h, blk)
 mv = torch.empty((n, 2), dtype=torch.int16, device="cuda")
 co = torch.empty(n, dtype=torch.int32, device="cuda")
+rows = sys.argv[2] if len(sys.argv) > 2 else ""
 for _ in range(5):
-    eng.full_search_device(rt, ct, blk, span, "sad", mv, co)
+    if rows:  # one stripe, planes resident whole (row offsets 0)
+        r0_, r1_ = (int(x) for x in rows.split(":"))
+        eng.search_stripe_device(rt, 0, ct, 0, w, h, blk, span, "sad", r0_, r1_, mv, co)
+    else:
+        eng.full_search_device(rt, ct, blk, span, "sad", mv, co)
 torch.cuda.synchronize()
 L = _lib.lib()
 L.me_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
@@ -41,6 +46,8 @@ dur = (st[:, 3] - st[:, 0]).astype(np.float64)
 print(f"{cfg}: {len(st)} persistent workgroups, items per WG min {items.min()} max {items.max()}")
 print(f"  WG lifetime cycles: min {dur.min():.0f} median {np.median(dur):.0f} max {dur.max():.0f}")
 print(f"  lifetime per item: median {np.median(dur / np.maximum(items, 1)):.0f}")
+stg = (st[:, 2] - st[:, 0]).astype(np.float64)
+print(f"  start -> first item staged (cycles): median {np.median(stg):.0f} p90 {np.percentile(stg, 90):.0f} max {stg.max():.0f}")
 for n in sorted(set(items.tolist())):
     sel = items == n
     print(f"  {n} items: {sel.sum()} WGs, median lifetime {np.median(dur[sel]):.0f}")
