@@ -25,6 +25,7 @@ Rank 0 prints ONE JSON line.
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import statistics
@@ -211,13 +212,13 @@ class StripeRun:
 
     Rank r holds its cur stripe and the ref rows with the S-row halo, searches
     its block rows (me_full_search_stripe_device), and sends its padded
-    records to rank 0 in one gather per frame.  With RCCL the gather is
-    asynchronous on RCCL's stream and the records are double-buffered: the
-    gather of frame k overlaps the search of frame k + 1, and the search of
-    frame k + 2 waits (on the GPU) for the gather that read its buffer."""
+    records to rank 0 in one gather per frame.  With RCCL the gather is the
+    library's ncclGather, enqueued right after the search on the same stream:
+    the host never waits inside the timed region."""
 
     def __init__(self, eng, dev, world, rank, gloo, ref, cur, blk, span, cost):
         import torch
+        import torch.distributed as dist
         from motionestimation_amd import shard
         h, w = ref.shape
         self.eng, self.dev, self.world, self.rank, self.gloo = eng, dev, world, rank, gloo
@@ -229,44 +230,60 @@ class StripeRun:
         self.recs = [torch.zeros((2, st.max_blocks), dtype=torch.int32, device=dev)
                      for _ in range(2)]
         cdev = torch.device("cpu") if gloo else dev
-        self.bufs = [[torch.empty_like(r, device=cdev) for _ in range(world)] if rank == 0
-                     else None for r in self.recs]
-        self.works = [None, None]
         self.i = 0
+        # RCCL ranks gather in libme_hip (me_gather_device) on the search's own
+        # stream, through calls marshalled once: a small stripe's step is bound
+        # by host time.  torch.distributed.gather cost ~30 us of host time per
+        # call, and a side stream's event handshake ~15 us more than it saves
+        # (the persistent search kernel holds every CU, so the gather cannot run
+        # beside it): 8-way 1080p stripe step 36-49 us -> 25-28 us on one GPU
+        # (profiles/r02au_step_overhead.jsonl, r02aw_step_overhead_same_stream.jsonl).
+        self.lib = world > 1 and not gloo
+        mvs = [r[0].view(torch.int16).view(st.max_blocks, 2) for r in self.recs]
+        self.run_search = [eng.prepared_stripe_search(
+            self.ref_t, st.ref_y0, self.cur_t, st.cur_y0, w, h, blk, span, cost, st.row_begin,
+            st.row_end, mvs[k], self.recs[k][1]) if st.nblocks else (lambda: None)
+            for k in range(2)]
+        if self.lib:
+            if not getattr(eng, "comm_ranks", 0):
+                uid = torch.zeros(128, dtype=torch.uint8, device=dev)
+                if rank == 0:
+                    uid.copy_(torch.frombuffer(bytearray(eng.comm_unique_id()), dtype=torch.uint8))
+                dist.broadcast(uid, 0)
+                eng.comm_init(bytes(uid.cpu().numpy().tobytes()), world, rank)
+                eng.comm_ranks = world
+            self.flat = [torch.empty((world,) + tuple(r.shape), dtype=r.dtype, device=dev)
+                         if rank == 0 else None for r in self.recs]
+            self.bufs = [list(f) if f is not None else None for f in self.flat]
+            self.run_gather = [eng.prepared_gather(self.recs[k], self.flat[k]) for k in range(2)]
+        else:
+            self.bufs = [[torch.empty_like(r, device=cdev) for _ in range(world)] if rank == 0
+                         else None for r in self.recs]
 
     def step(self):
-        import torch
         import torch.distributed as dist
         k = self.i & 1
         self.i += 1
-        rec, st = self.recs[k], self.st
-        if self.works[k] is not None:  # the gather that read recs[k] (frame i - 2)
-            self.works[k].wait()       # RCCL: the current stream waits, not the host
-            self.works[k] = None
-        if st.nblocks:
-            mv = rec[0].view(torch.int16).view(st.max_blocks, 2)  # (mvx, mvy) int16 pairs
-            self.eng.search_stripe_device(self.ref_t, st.ref_y0, self.cur_t, st.cur_y0, self.w,
-                                          self.h, self.blk, self.span, self.cost, st.row_begin,
-                                          st.row_end, mv, rec[1])
-        if self.world > 1:  # the one exchange: per-stripe MV records -> rank 0
-            if self.gloo:
-                dist.gather(rec.cpu(), self.bufs[k], dst=0)
-            else:
-                self.works[k] = dist.gather(rec, self.bufs[k], dst=0, async_op=True)
+        if self.lib:  # search, then the one exchange, in stream order (no host sync)
+            self.run_search[k]()
+            self.run_gather[k]()
+            return k
+        self.run_search[k]()
+        if self.world > 1:  # gloo rehearsal: per-stripe MV records -> rank 0
+            dist.gather(self.recs[k].cpu(), self.bufs[k], dst=0)
         return k
 
-    def drain(self):
-        for k in range(2):
-            if self.works[k] is not None:
-                self.works[k].wait()
-                self.works[k] = None
+    def gather_impl(self):
+        if self.world == 1:
+            return None
+        return ("me_gather_device (RCCL ncclGather in libme_hip, on the search stream)" if self.lib else
+                "torch.distributed.gather (gloo rehearsal)")
 
     def gathered_field(self):
         """A last, synchronous frame; rank 0 returns the assembled (mv, cost)."""
         import torch
         from motionestimation_amd import shard
         k = self.step()
-        self.drain()
         torch.cuda.synchronize()
         if self.rank != 0:
             return None
@@ -340,7 +357,7 @@ def stripe_record(eng, dev, world, rank, gloo, cfg_name, cost, steps, warmup):
     ref, cur = synth.frame_pair(w, h, seed, sx, sy)
     cands = me.candidate_count(w, h, blk, span)
     sr = StripeRun(eng, dev, world, rank, gloo, ref, cur, blk, span, cost)
-    elapsed, kern_ms = timed(sr.step, steps, warmup, world, sr.drain)
+    elapsed, kern_ms = timed(sr.step, steps, warmup, world)
     parity = stripe_parity(eng, sr, ref, cur, dev)
     return {"value": cands * steps / elapsed, "unit": "candidates/s",
             "frames_per_s": steps / elapsed, "ms_per_step": elapsed / steps * 1e3,
@@ -348,7 +365,8 @@ def stripe_record(eng, dev, world, rank, gloo, cfg_name, cost, steps, warmup):
             "scaling": "strong", "parallelism": f"stripe{world}",
             "workload": f"{w}x{h} Y, {blk}x{blk} blocks, full search +-{span}, {cost.upper()}, "
                         "one frame per step in row stripes + one RCCL gather per frame",
-            "candidates_per_frame": cands, "stripe_gather_parity": parity}
+            "candidates_per_frame": cands, "stripe_gather_parity": parity,
+            "gather": sr.gather_impl()}
 
 
 def load_traffic(tag):
@@ -416,7 +434,7 @@ def main():
         sr = StripeRun(eng, dev, world, rank, gloo, ref, cur, blk, span, args.cost)
         st = sr.st
         units_per_step = cands_frame
-        elapsed, kern_ms = timed(sr.step, args.steps, args.warmup, world, sr.drain)
+        elapsed, kern_ms = timed(sr.step, args.steps, args.warmup, world)
         parity = stripe_parity(eng, sr, ref, cur, dev)
 
     value = units_per_step * args.steps / elapsed
@@ -485,6 +503,7 @@ def main():
                                       min(args.steps, 20))
     if parity is not None:
         line["stripe_gather_parity"] = parity
+        line["config"]["gather"] = sr.gather_impl()
     if rank == 0 and world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baselines(ref, cur, blk, span, args.cost, args.cpu_threads,
                                              cands_frame)

@@ -146,6 +146,23 @@ me_status me_full_search_stripe_device(me_ctx* ctx, const uint8_t* d_ref,
 me_status me_plan_stripes(int width, int height, int block_size,
                           int search_range, int n_shards, int* bounds);
 
+/* ---- multi-process stripes (one process per GPU) ----
+ * The one exchange step of a sharded search, issued from C so a rank's step
+ * costs two native calls instead of a Python collective.  Rank 0 calls
+ * me_comm_unique_id and sends the ME_COMM_ID_BYTES bytes to the other ranks
+ * out of band (e.g. a torch.distributed broadcast); every rank then calls
+ * me_comm_init with them (collective: all ranks at once) to build an RCCL
+ * communicator on ctx's first device.  No reference counterpart: the
+ * reference is single-process. */
+#define ME_COMM_ID_BYTES 128
+me_status me_comm_unique_id(void* id);
+me_status me_comm_init(me_ctx* ctx, const void* id, int n_ranks, int rank);
+/* Gather `bytes` from every rank's device buffer d_send into rank 0's d_recv
+ * (n_ranks * bytes, rank order; d_recv is ignored on other ranks), enqueued on
+ * `stream` (a hipStream_t) after the work already on it; asynchronous. */
+me_status me_gather_device(me_ctx* ctx, const void* d_send, size_t bytes, void* d_recv,
+                           void* stream);
+
 /* Reference block record, field for field src/common/block.h:6-19 (44 B). */
 typedef struct me_ref_block {
   int idx_x, idx_y;

@@ -16,6 +16,7 @@ if os.environ.get("ME_HIP_LIB"):
 CSRC = os.path.join(PKG, "csrc")
 
 ME_OK, ME_EINVAL, ME_ENOMEM, ME_EDEVICE, ME_ECOMM, ME_EUNSUPPORTED, ME_EIO = range(7)
+ME_COMM_ID_BYTES = 128  # include/me.h (sizeof ncclUniqueId)
 ME_YUV_LUMA, ME_YUV_I420 = 0, 1
 ME_COST_SSD, ME_COST_SAD, ME_COST_SSIM = 0, 1, 2
 ME_PATH_AUTO, ME_PATH_VALU, ME_PATH_MFMA_TILES = 0, 1, 2
@@ -41,6 +42,10 @@ _SIGS = {
                                                     ctypes.c_int] + [ctypes.c_int] * 8 +
                                      [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "me_plan_stripes": (ctypes.c_int, [ctypes.c_int] * 5 + [ctypes.POINTER(ctypes.c_int)]),
+    "me_comm_unique_id": (ctypes.c_int, [ctypes.c_void_p]),
+    "me_comm_init": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
+    "me_gather_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                        ctypes.c_void_p, ctypes.c_void_p]),
     "me_find_best_blocks": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p] +
                             [ctypes.c_int] * 4 + [ctypes.c_void_p, ctypes.c_int]),
     "me_motion_compensate": (ctypes.c_int, [ctypes.c_void_p, _u8p] + [ctypes.c_int] * 3 +

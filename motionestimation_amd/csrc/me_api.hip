@@ -492,8 +492,48 @@ me_status me_create(me_ctx** out, const int* device_ids, int n) {
   return ME_OK;
 }
 
+me_status me_comm_unique_id(void* id) {
+  if (!id) return ME_EINVAL;
+  static_assert(sizeof(ncclUniqueId) == ME_COMM_ID_BYTES, "ncclUniqueId size");
+  ncclUniqueId u;
+  if (ncclGetUniqueId(&u) != ncclSuccess) return ME_ECOMM;
+  memcpy(id, &u, sizeof(u));
+  return ME_OK;
+}
+
+me_status me_comm_init(me_ctx* c, const void* id, int n_ranks, int rank) {
+  if (!c) return ME_EINVAL;
+  if (!id || n_ranks < 1 || rank < 0 || rank >= n_ranks)
+    return fail(c, ME_EINVAL, "comm rank %d of %d", rank, n_ranks);
+  if (c->rank_comm) return fail(c, ME_EINVAL, "communicator already initialised");
+  ncclUniqueId u;
+  memcpy(&u, id, sizeof(u));
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  HIPCHK(c, hipSetDevice(c->devs[0].id));
+  ncclComm_t comm = nullptr;
+  const ncclResult_t r = ncclCommInitRank(&comm, n_ranks, u, rank);
+  (void)hipSetDevice(prev);
+  if (r != ncclSuccess) return fail(c, ME_ECOMM, "ncclCommInitRank: %s", ncclGetErrorString(r));
+  c->rank_comm = comm;
+  c->comm_ranks = n_ranks;
+  c->comm_rank = rank;
+  return ME_OK;
+}
+
+me_status me_gather_device(me_ctx* c, const void* d_send, size_t bytes, void* d_recv,
+                           void* stream) {
+  if (!c) return ME_EINVAL;
+  if (!c->rank_comm) return fail(c, ME_EINVAL, "me_comm_init was not called");
+  if (!d_send || (c->comm_rank == 0 && !d_recv)) return fail(c, ME_EINVAL, "null buffer");
+  NCCLCHK(c, ncclGather(d_send, c->comm_rank == 0 ? d_recv : nullptr, bytes, ncclUint8, 0,
+                        c->rank_comm, reinterpret_cast<hipStream_t>(stream)));
+  return ME_OK;
+}
+
 void me_destroy(me_ctx* c) {
   if (!c) return;
+  if (c->rank_comm) ncclCommDestroy(c->rank_comm);
   if (c->comms) {
     for (size_t i = 0; i < c->devs.size(); i++) ncclCommDestroy(c->comms[i]);
     delete[] c->comms;

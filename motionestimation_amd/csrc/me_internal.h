@@ -89,6 +89,8 @@ struct me_ctx {
   std::vector<me::Dev> devs;
   bool distinct = true;
   ncclComm_t* comms = nullptr;
+  ncclComm_t rank_comm = nullptr;  // me_comm_init: one rank of a multi-process group
+  int comm_ranks = 0, comm_rank = -1;
   char err[512] = {0};
 };
 

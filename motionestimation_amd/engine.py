@@ -179,6 +179,65 @@ class Engine:
             cost_t.data_ptr() if cost_t is not None else None, st), self._h)
 
 
+    # ---- multi-process stripes: the one exchange step in native code ----
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        """RCCL unique id (rank 0), to be sent to every rank out of band."""
+        buf = ctypes.create_string_buffer(_lib.ME_COMM_ID_BYTES)
+        check(_lib.lib().me_comm_unique_id(buf))
+        return buf.raw
+
+    def comm_init(self, uid: bytes, n_ranks: int, rank: int) -> None:
+        """Join an n_ranks RCCL group on this context's first device (collective)."""
+        if len(uid) != _lib.ME_COMM_ID_BYTES:
+            raise ValueError(f"comm id of {len(uid)} bytes, expected {_lib.ME_COMM_ID_BYTES}")
+        check(_lib.lib().me_comm_init(self._h, uid, n_ranks, rank), self._h)
+
+    def gather_device(self, send_t, recv_t=None, stream=None) -> None:
+        """Gather send_t (same byte count on every rank) into rank 0's recv_t
+        (n_ranks x the bytes, rank order), enqueued on `stream` (default: torch's
+        current stream)."""
+        st = stream if stream is not None else _current_stream()
+        check(_lib.lib().me_gather_device(
+            self._h, send_t.data_ptr(), send_t.numel() * send_t.element_size(),
+            recv_t.data_ptr() if recv_t is not None else None, st), self._h)
+
+
+    # ---- prepared calls: arguments marshalled once per buffer set ----
+    # A sharded step on a small stripe is bound by host time (an 8-way 1080p
+    # stripe searches in 15-18 us), so the per-frame calls skip the wrapper's
+    # argument handling.  The caller keeps the tensors alive.
+    def prepared_stripe_search(self, ref_t, ref_row0, cur_t, cur_row0, width, height, blk,
+                               span, cost, row_begin, row_end, mv_t, cost_t, stream=None,
+                               stride=None):
+        """Zero-argument callable enqueueing search_stripe_device(...) with these
+        fixed buffers on `stream` (default: torch's current stream now)."""
+        fn, h = _lib.lib().me_full_search_stripe_device, self._h
+        args = (h, ref_t.data_ptr(), ref_row0, cur_t.data_ptr(), cur_row0, width, height,
+                stride or width, blk, span, cost_code(cost), row_begin, row_end,
+                mv_t.data_ptr(), cost_t.data_ptr() if cost_t is not None else None,
+                stream if stream is not None else _current_stream())
+
+        def run():
+            s = fn(*args)
+            if s:
+                check(s, h)
+        return run
+
+    def prepared_gather(self, send_t, recv_t=None, stream=None):
+        """Zero-argument callable enqueueing gather_device(send_t, recv_t)."""
+        fn, h = _lib.lib().me_gather_device, self._h
+        args = (h, send_t.data_ptr(), send_t.numel() * send_t.element_size(),
+                recv_t.data_ptr() if recv_t is not None else None,
+                stream if stream is not None else _current_stream())
+
+        def run():
+            s = fn(*args)
+            if s:
+                check(s, h)
+        return run
+
+
 class _Pinned:
     """Owner of one me_host_alloc block (freed when the last view dies)."""
 

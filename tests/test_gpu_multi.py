@@ -80,6 +80,28 @@ def test_multi_device_context_rccl_gather():
                 np.testing.assert_array_equal(c, oc)
 
 
+def test_library_communicator_one_rank():
+    """me_comm_init / me_gather_device (bench.py's RCCL exchange step) with a
+    one-rank group: the gather lands the records bit for bit, on a side stream
+    ordered by events; gathering before init and a second init fail loudly."""
+    import torch
+    with me.Engine(devices=[0]) as eng:
+        src = torch.randint(-2**31, 2**31 - 1, (2, 1000), dtype=torch.int32, device="cuda")
+        dst = torch.zeros((1, 2, 1000), dtype=torch.int32, device="cuda")
+        with pytest.raises(me.MEError):
+            eng.gather_device(src, dst)
+        eng.comm_init(eng.comm_unique_id(), 1, 0)
+        with pytest.raises(me.MEError):
+            eng.comm_init(eng.comm_unique_id(), 1, 0)
+        gs = torch.cuda.Stream()
+        ev = torch.cuda.Event()
+        ev.record()
+        gs.wait_event(ev)
+        eng.gather_device(src, dst, stream=ctypes.c_void_p(gs.cuda_stream))
+        torch.cuda.synchronize()
+        assert torch.equal(dst[0], src)
+
+
 def _bench_ranks(nproc, backend, extra=()):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
            f"--nproc-per-node={nproc}", "--master-addr=127.0.0.1", "--master-port=29731",
@@ -114,6 +136,7 @@ def test_bench_stripe_mode_rccl():
     """The same over RCCL, one rank per GPU (asynchronous gathers overlapping
     the next frame's search)."""
     n = min(_ngpu(), 8)
-    _check_stripe_line(_bench_ranks(2, "nccl"), 2)
-    if n > 2:
-        _check_stripe_line(_bench_ranks(n, "nccl"), n)
+    for k in sorted({2, n}):
+        d = _bench_ranks(k, "nccl")
+        _check_stripe_line(d, k)
+        assert "me_gather_device" in d["config"]["gather"]

@@ -6,13 +6,15 @@ bound by the host: the ctypes search launch plus the RCCL gather call.  This
 times, for one rank's stripe of an N-way split on ONE GPU, K back-to-back steps
 of (a) the search alone, (b) search + async RCCL gather (double-buffered
 records, as bench.py's StripeRun) in a world-size-1 RCCL group, and (c) the
-gather alone, and prints one JSON line per case: wall us per step against HIP-event us per step.
+gather alone, (d) search + the library's gather (me_gather_device, as
+bench.py's RCCL ranks), and prints one JSON line per case: wall us per step against HIP-event us per step.
 
   python tools/step_overhead.py [--config 1080p] [--ways 8] [--rank 1] [--steps 2000]
 """
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -110,6 +112,64 @@ def main():
         works[k] = dist.gather(recs[k], bufs[k], dst=0, async_op=True)
 
     run("gather", step_gather_only, a.steps, drain)
+
+    # (d) bench.py's RCCL path: the gather in libme_hip (me_gather_device) on a
+    # side stream, ordered by events (a world-size-1 library communicator)
+    eng.comm_init(eng.comm_unique_id(), 1, 0)
+    gs = torch.cuda.Stream(dev)
+    gs_h = ctypes.c_void_p(gs.cuda_stream)
+    sev = [torch.cuda.Event() for _ in range(2)]
+    gev = [torch.cuda.Event() for _ in range(2)]
+    flat = [torch.empty((1,) + tuple(r.shape), dtype=r.dtype, device=dev) for r in recs]
+    pend = [False, False]
+
+    def step_libgather():
+        k = state["i"] & 1
+        state["i"] += 1
+        cur_s = torch.cuda.current_stream()
+        if pend[k]:
+            cur_s.wait_event(gev[k])
+        search(recs[k])
+        sev[k].record(cur_s)
+        gs.wait_event(sev[k])
+        eng.gather_device(recs[k], flat[k], stream=gs_h)
+        gev[k].record(gs)
+        pend[k] = True
+
+    def libdrain():
+        for k in range(2):
+            if pend[k]:
+                torch.cuda.current_stream().wait_event(gev[k])
+                pend[k] = False
+
+    run("search+libgather", step_libgather, a.steps, libdrain)
+
+    def step_libgather_same():  # the gather on the search's own stream, no events
+        k = state["i"] & 1
+        state["i"] += 1
+        search(recs[k])
+        eng.gather_device(recs[k], flat[k])
+
+    run("search+libgather_same_stream", step_libgather_same, a.steps)
+
+    # (e) bench.py's StripeRun: the same two calls, marshalled once
+    mvs = [r[0].view(torch.int16).view(st.max_blocks, 2) for r in recs]
+    ps = [eng.prepared_stripe_search(ref_t, st.ref_y0, cur_t, st.cur_y0, w, h, blk, span, "sad",
+                                     st.row_begin, st.row_end, mvs[k], recs[k][1])
+          for k in range(2)]
+    pg = [eng.prepared_gather(recs[k], flat[k]) for k in range(2)]
+
+    def step_prepared():
+        k = state["i"] & 1
+        state["i"] += 1
+        ps[k]()
+        pg[k]()
+
+    run("prepared_search+libgather", step_prepared, a.steps)
+    run("prepared_search", lambda: ps[0](), a.steps)
+    torch.cuda.synchronize()
+    ok = all(torch.equal(flat[k][0], recs[k]) for k in range(2))
+    print(json.dumps({"case": "libgather_parity", "equal": ok}), flush=True)
     dist.destroy_process_group()
     eng.close()
 
