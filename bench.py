@@ -245,13 +245,12 @@ class StripeRun:
             st.row_end, mvs[k], self.recs[k][1]) if st.nblocks else (lambda: None)
             for k in range(2)]
         if self.lib:
-            if not getattr(eng, "comm_ranks", 0):
+            if not eng.comm_ranks:  # one communicator per context (stripe_4k reuses it)
                 uid = torch.zeros(128, dtype=torch.uint8, device=dev)
                 if rank == 0:
                     uid.copy_(torch.frombuffer(bytearray(eng.comm_unique_id()), dtype=torch.uint8))
                 dist.broadcast(uid, 0)
                 eng.comm_init(bytes(uid.cpu().numpy().tobytes()), world, rank)
-                eng.comm_ranks = world
             self.flat = [torch.empty((world,) + tuple(r.shape), dtype=r.dtype, device=dev)
                          if rank == 0 else None for r in self.recs]
             self.bufs = [list(f) if f is not None else None for f in self.flat]

@@ -74,6 +74,7 @@ class Engine:
         check(st)
         self._h = h
         self.devices = list(devices) if devices else None
+        self.comm_ranks = 0  # me_comm_init: size of this context's RCCL group
 
     def close(self) -> None:
         if getattr(self, "_h", None):
@@ -192,6 +193,7 @@ class Engine:
         if len(uid) != _lib.ME_COMM_ID_BYTES:
             raise ValueError(f"comm id of {len(uid)} bytes, expected {_lib.ME_COMM_ID_BYTES}")
         check(_lib.lib().me_comm_init(self._h, uid, n_ranks, rank), self._h)
+        self.comm_ranks = n_ranks
 
     def gather_device(self, send_t, recv_t=None, stream=None) -> None:
         """Gather send_t (same byte count on every rank) into rank 0's recv_t
