@@ -238,7 +238,9 @@ class StripeRun:
         # (the persistent search kernel holds every CU, so the gather cannot run
         # beside it): 8-way 1080p stripe step 36-49 us -> 25-28 us on one GPU
         # (profiles/r02au_step_overhead.jsonl, r02aw_step_overhead_same_stream.jsonl).
-        self.lib = world > 1 and not gloo
+        # (a one-rank RCCL group under torch.distributed.run takes this path too:
+        # the GPU test of the library gather on a one-GPU box)
+        self.lib = dist.is_initialized() and not gloo
         mvs = [r[0].view(torch.int16).view(st.max_blocks, 2) for r in self.recs]
         self.run_search = [eng.prepared_stripe_search(
             self.ref_t, st.ref_y0, self.cur_t, st.cur_y0, w, h, blk, span, cost, st.row_begin,
@@ -273,7 +275,7 @@ class StripeRun:
         return k
 
     def gather_impl(self):
-        if self.world == 1:
+        if self.world == 1 and not self.lib:
             return None
         return ("me_gather_device (RCCL ncclGather in libme_hip, on the search stream)" if self.lib else
                 "torch.distributed.gather (gloo rehearsal)")
@@ -286,7 +288,7 @@ class StripeRun:
         torch.cuda.synchronize()
         if self.rank != 0:
             return None
-        if self.world == 1:
+        if self.world == 1 and not self.lib:
             rec = self.recs[k].cpu()
             return shard.assemble([rec], self.stripes)
         return shard.assemble(self.bufs[k], self.stripes)
@@ -396,7 +398,10 @@ def main():
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
     gloo = args.dist_backend == "gloo"
-    if world > 1:
+    # a process group whenever torch.distributed.run launched us (WORLD_SIZE set),
+    # a one-rank group included
+    launched = "WORLD_SIZE" in os.environ
+    if launched:
         if gloo:
             dist.init_process_group("gloo")
         else:
@@ -519,7 +524,7 @@ def main():
     if rank == 0:
         print(json.dumps(line), flush=True)
     eng.close()
-    if world > 1:
+    if launched:
         dist.destroy_process_group()
 
 

@@ -131,6 +131,17 @@ def test_bench_stripe_mode_two_ranks_gloo_rehearsal():
     _check_stripe_line(_bench_ranks(2, "gloo"), 2)
 
 
+def test_bench_stripe_mode_rccl_one_rank():
+    """bench.py's RCCL stripe path end to end on one GPU: torch.distributed.run
+    with one rank, the unique id broadcast, me_comm_init, and every frame's
+    me_gather_device (1080p and the nested 4K record), gathered fields equal to
+    a full-frame search."""
+    d = _bench_ranks(1, "nccl", ("--mode", "stripe"))
+    _check_stripe_line(d, 1)
+    assert "me_gather_device" in d["config"]["gather"]
+    assert "me_gather_device" in d["stripe_4k"]["gather"]
+
+
 @pytest.mark.skipif("_ngpu() < 2", reason="needs >= 2 GPUs (one RCCL rank per GPU)")
 def test_bench_stripe_mode_rccl():
     """The same over RCCL, one rank per GPU (asynchronous gathers overlapping
