@@ -385,6 +385,11 @@ def load_traffic(tag):
 
 def main():
     args = parse()
+    # stdout carries exactly the one JSON line: anything else written to fd 1
+    # (RCCL's version banner at communicator init, library messages) goes to stderr
+    sys.stdout.flush()
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     import torch
     import torch.distributed as dist
 
@@ -522,7 +527,7 @@ def main():
         line["host_stream"] = host_stream(eng, w, h, blk, span, args.cost, seed, sx, sy,
                                           kern_ms, cands_frame)
     if rank == 0:
-        print(json.dumps(line), flush=True)
+        print(json.dumps(line), file=json_out, flush=True)
     eng.close()
     if launched:
         dist.destroy_process_group()
