@@ -236,8 +236,8 @@ class StripeRun:
         # by host time.  torch.distributed.gather cost ~30 us of host time per
         # call, and a side stream's event handshake ~15 us more than it saves
         # (the persistent search kernel holds every CU, so the gather cannot run
-        # beside it): 8-way 1080p stripe step 36-49 us -> 25-28 us on one GPU
-        # (profiles/r02au_step_overhead.jsonl, r02aw_step_overhead_same_stream.jsonl).
+        # beside it): 8-way 1080p stripe step 36-49 us -> 21-24 us on one GPU
+        # (profiles/r02au_step_overhead.jsonl ... r02ax_step_overhead_prepared.jsonl).
         # (a one-rank RCCL group under torch.distributed.run takes this path too:
         # the GPU test of the library gather on a one-GPU box)
         self.lib = dist.is_initialized() and not gloo
