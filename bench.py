@@ -19,7 +19,11 @@ HBM before the timed region.
   each rank searches its own frame pair per step: weak scaling, no collective.
 Every line also carries `stripe_4k`: BASELINE configs[3] (4K +-64) in stripe
 mode on the same ranks, with its gather parity.
-For N > 1 launch with torch.distributed.run (one process per GPU, RCCL).
+For N > 1: one process per GPU over RCCL.  Under torch.distributed.run
+(WORLD_SIZE set) the ranks are the launcher's; without a launcher bench.py
+starts `torch.distributed.run --nproc-per-node N` itself as a child before
+anything touches the GPU and forwards its line (launch_ranks; fewer visible
+GPUs than RCCL ranks is an error, never an n_gpus = 1 line).
 Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
@@ -67,6 +71,9 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16,
                     help="threads of the main CPU-baseline leg (the GPU box's CPU share)")
     ap.add_argument("--no-4k", action="store_true", help="skip the nested stripe_4k record")
+    ap.add_argument("--no-graph", action="store_true",
+                    help="stripe mode over RCCL: enqueue search + gather per frame instead of "
+                         "replaying one captured hipGraph")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="nccl = RCCL (production); gloo only to rehearse N ranks on one GPU")
     return ap.parse_args()
@@ -79,6 +86,22 @@ def _block_candidates(w, h, blk, span, bx, by):
     nx = min(span, w - bw - tlx) - max(-span, -tlx) + 1
     ny = min(span, h - bh - tly) - max(-span, -tly) + 1
     return nx * ny
+
+
+def exact_absdiffs(w, h, blk, span, row0=0, row1=None):
+    """Exact |a-b| (or multiply-add) count of block rows [row0, row1): every
+    block's candidates (main.c:53-54, 73-76) times its own w*h pixels (edge
+    blocks are partial, prediction_frame.c:21-22).  1080p 16x16 +-32:
+    8,463,799,296."""
+    nbx, nby = (w + blk - 1) // blk, (h + blk - 1) // blk
+    row1 = nby if row1 is None else row1
+    bx = np.arange(nbx, dtype=np.int64)
+    by = np.arange(row0, row1, dtype=np.int64)
+    tlx, tly = bx * blk, by * blk
+    bw, bh = np.minimum(blk, w - tlx), np.minimum(blk, h - tly)
+    nx = np.minimum(span, w - bw - tlx) - np.maximum(-span, -tlx) + 1
+    ny = np.minimum(span, h - bh - tly) - np.maximum(-span, -tly) + 1
+    return int((nx * bw).sum() * (ny * bh).sum())
 
 
 def cpu_baselines(ref, cur, blk, span, cost, threads, cands):
@@ -200,7 +223,8 @@ def ssd_beside(eng, ref_t, cur_t, blk, span, nb, cands_frame, dev, steps):
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / steps
-    tops = 2.0 * blk * blk * cands_frame / (ms / 1e3) / 1e12
+    h, w = ref_t.shape
+    tops = 2.0 * exact_absdiffs(w, h, blk, span) / (ms / 1e3) / 1e12
     return {"value": cands_frame / (ms / 1e3), "unit": "candidates/s", "kernel_ms": ms,
             "steps": steps, "cost": "ssd (reference MSE argmin, bit-exact)",
             "roofline": {"bound": "mfma", "achieved": tops, "peak": I8_PEAK_TOPS,
@@ -216,7 +240,7 @@ class StripeRun:
     library's ncclGather, enqueued right after the search on the same stream:
     the host never waits inside the timed region."""
 
-    def __init__(self, eng, dev, world, rank, gloo, ref, cur, blk, span, cost):
+    def __init__(self, eng, dev, world, rank, gloo, ref, cur, blk, span, cost, graph=True):
         import torch
         import torch.distributed as dist
         from motionestimation_amd import shard
@@ -257,6 +281,28 @@ class StripeRun:
                          if rank == 0 else None for r in self.recs]
             self.bufs = [list(f) if f is not None else None for f in self.flat]
             self.run_gather = [eng.prepared_gather(self.recs[k], self.flat[k]) for k in range(2)]
+            # One hipGraph per record buffer holding the search and its gather
+            # (me_capture_begin/end): a frame is one graph launch instead of two
+            # enqueues (the search call ~6 us and ncclGather's ~14 us of host
+            # time made the 8-way 1080p step host-bound).  Each is
+            # run once uncaptured first: that sizes the search scratch and sets
+            # up RCCL's connections.
+            self.graphs = None
+            if graph and st.nblocks:
+                from motionestimation_amd import MEError
+                stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+                for k in range(2):
+                    self.run_search[k]()
+                    self.run_gather[k]()
+                torch.cuda.synchronize()
+                try:
+                    self.graphs = [eng.capture(stream, lambda k=k: (self.run_search[k](),
+                                                                     self.run_gather[k]()))
+                                   for k in range(2)]
+                    self.run_graph = [g.prepared(stream) for g in self.graphs]
+                except MEError as e:  # reported in the line (config.gather)
+                    print(f"bench.py: graph capture failed, direct enqueue: {e}", file=sys.stderr)
+                    self.graphs = None
         else:
             self.bufs = [[torch.empty_like(r, device=cdev) for _ in range(world)] if rank == 0
                          else None for r in self.recs]
@@ -266,6 +312,9 @@ class StripeRun:
         k = self.i & 1
         self.i += 1
         if self.lib:  # search, then the one exchange, in stream order (no host sync)
+            if self.graphs:
+                self.run_graph[k]()
+                return k
             self.run_search[k]()
             self.run_gather[k]()
             return k
@@ -277,8 +326,11 @@ class StripeRun:
     def gather_impl(self):
         if self.world == 1 and not self.lib:
             return None
-        return ("me_gather_device (RCCL ncclGather in libme_hip, on the search stream)" if self.lib else
-                "torch.distributed.gather (gloo rehearsal)")
+        if not self.lib:
+            return "torch.distributed.gather (gloo rehearsal)"
+        return ("me_gather_device (RCCL ncclGather in libme_hip, on the search stream)" +
+                (", search + gather captured in one hipGraph per record buffer"
+                 if getattr(self, "graphs", None) else ""))
 
     def gathered_field(self):
         """A last, synchronous frame; rank 0 returns the assembled (mv, cost)."""
@@ -349,7 +401,7 @@ def stripe_parity(eng, sr, ref, cur, dev):
                 np.array_equal(gcost, fco.cpu().numpy().view(np.uint32)))
 
 
-def stripe_record(eng, dev, world, rank, gloo, cfg_name, cost, steps, warmup):
+def stripe_record(eng, dev, world, rank, gloo, cfg_name, cost, steps, warmup, graph=True):
     """Nested record: a BASELINE config in stripe mode on the same ranks."""
     import motionestimation_amd as me
     from motionestimation_amd import synth
@@ -357,7 +409,7 @@ def stripe_record(eng, dev, world, rank, gloo, cfg_name, cost, steps, warmup):
     w, h, seed, sx, sy = synth.CONFIGS[cfg]
     ref, cur = synth.frame_pair(w, h, seed, sx, sy)
     cands = me.candidate_count(w, h, blk, span)
-    sr = StripeRun(eng, dev, world, rank, gloo, ref, cur, blk, span, cost)
+    sr = StripeRun(eng, dev, world, rank, gloo, ref, cur, blk, span, cost, graph)
     elapsed, kern_ms = timed(sr.step, steps, warmup, world)
     parity = stripe_parity(eng, sr, ref, cur, dev)
     return {"value": cands * steps / elapsed, "unit": "candidates/s",
@@ -383,8 +435,56 @@ def load_traffic(tag):
         return None, None
 
 
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args):
+    """`bench.py --gpus N` (N > 1) with no launcher: start N ranks, one process
+    per GPU, as a child `torch.distributed.run` and forward rank 0's JSON line.
+
+    Runs before anything touches the GPU (torch.cuda.device_count() does not
+    initialise it on this image), so the parent never holds a device while its
+    child runs.  Refuses, with a non-zero exit and no JSON line, a request for
+    more RCCL ranks than visible devices (gloo ranks may share one GPU: the
+    rehearsal mode)."""
+    import torch
+    ndev = torch.cuda.device_count()
+    if args.dist_backend == "nccl" and ndev < args.gpus:
+        print(f"bench.py: --gpus {args.gpus} needs {args.gpus} visible GPUs, found {ndev}",
+              file=sys.stderr)
+        return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1",
+           f"--master-port={_free_port()}", os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, env=env, text=True)
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    for l in r.stdout.splitlines():
+        if not l.startswith("{"):
+            print(l, file=sys.stderr)
+    if r.returncode != 0 or len(lines) != 1:
+        print(f"bench.py: {args.gpus}-rank child exited {r.returncode} with {len(lines)} JSON "
+              "lines", file=sys.stderr)
+        return r.returncode or 3
+    d = json.loads(lines[0])
+    if d.get("n_gpus") != args.gpus:
+        print(f"bench.py: child reported n_gpus {d.get('n_gpus')}", file=sys.stderr)
+        return 3
+    print(lines[0], flush=True)
+    return 0
+
+
 def main():
     args = parse()
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     # stdout carries exactly the one JSON line: anything else written to fd 1
     # (RCCL's version banner at communicator init, library messages) goes to stderr
     sys.stdout.flush()
@@ -396,13 +496,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.gpus != world and world > 1:
+    if args.gpus != world:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
     ndev = torch.cuda.device_count()
+    gloo = args.dist_backend == "gloo"
+    if ndev < 1 or (not gloo and ndev < world):
+        raise SystemExit(f"{world} RCCL ranks need {world} visible GPUs, found {ndev}")
     gpu = local % ndev  # ranks > devices only in a gloo rehearsal on one GPU
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
-    gloo = args.dist_backend == "gloo"
+    # Every search of the run goes on one created stream (graph capture needs
+    # one; the legacy NULL stream cannot be captured), and the HIP events that
+    # time the kernels are recorded on it (torch's current stream).
+    torch.cuda.set_stream(torch.cuda.Stream(device=dev))
     # a process group whenever torch.distributed.run launched us (WORLD_SIZE set),
     # a one-rank group included
     launched = "WORLD_SIZE" in os.environ
@@ -440,7 +546,8 @@ def main():
         elapsed, kern_ms = timed(step, args.steps, args.warmup, world)
     else:
         ref, cur = synth.frame_pair(w, h, seed, sx, sy)
-        sr = StripeRun(eng, dev, world, rank, gloo, ref, cur, blk, span, args.cost)
+        sr = StripeRun(eng, dev, world, rank, gloo, ref, cur, blk, span, args.cost,
+                       not args.no_graph)
         st = sr.st
         units_per_step = cands_frame
         elapsed, kern_ms = timed(sr.step, args.steps, args.warmup, world)
@@ -450,12 +557,14 @@ def main():
     # Roofline of the dominant kernel: algorithmic HBM bytes per
     # launch = 2*W*H (u8 ref + cur, read once) + 8*nblocks (mv + cost written)
     # for the planes that launch covers.
+    # VALU work: the exact abs-diff count (w*h of each block, not B*B).
+    # Stripe mode: the frame's work / N against the slowest rank's kernel time.
     if mode == "frames":
         alg_bytes = 2 * w * h + 8 * nb
-        absdiffs = cands_frame * blk * blk
+        absdiffs = exact_absdiffs(w, h, blk, span)
     else:
         alg_bytes = (st.ref_y1 - st.ref_y0 + st.cur_y1 - st.cur_y0) * w + 8 * st.nblocks
-        absdiffs = cands_frame * blk * blk / world
+        absdiffs = exact_absdiffs(w, h, blk, span) / world
     achieved = alg_bytes / (kern_ms / 1e3) / 1e9
     tag = f"{args.config}_b{blk}_s{span}_{args.cost}"
     traffic, traffic_search = load_traffic(tag)
@@ -495,14 +604,14 @@ def main():
     if args.cost == "ssd" and blk in (8, 16):
         # B = 8 and 16 SSD run on the matrix cores (i8 MFMA cross term): the bound is
         # the MFMA peak; algorithmic ops = 2 x B*B multiply-adds per candidate
-        ops = 2.0 * blk * blk * (cands_frame if mode == "frames" else cands_frame / world)
+        ops = 2.0 * absdiffs
         tops = ops / (kern_ms / 1e3) / 1e12
         hbm = line["roofline"]
         hbm.pop("valu", None)
         line["roofline"] = {"bound": "mfma", "achieved": tops, "peak": I8_PEAK_TOPS,
                             "unit": "TFLOP/s", "frac": tops / I8_PEAK_TOPS, "traffic": traffic,
                             "traffic_per_search": traffic_search,
-                            "note": "useful int8 ops (2*B*B per candidate) over the whole search "
+                            "note": "useful int8 ops (2*w*h per candidate) over the whole search "
                                     "(S2 prepass + MFMA kernel); dense i8 peak",
                             "hbm": {k: hbm[k] for k in ("achieved", "peak", "unit", "frac",
                                                         "algorithmic_bytes_per_launch")}}
@@ -520,7 +629,7 @@ def main():
         # BASELINE configs[3] (4K +-64), the config north_star's 8-GPU split is
         # quoted on, in stripe mode on the same ranks (at N = 1: the denominator)
         rec4k = stripe_record(eng, dev, world, rank, gloo, "4k", args.cost,
-                              min(args.steps, 20), min(args.warmup, 3))
+                              min(args.steps, 20), min(args.warmup, 3), not args.no_graph)
         if rank == 0:
             line["stripe_4k"] = rec4k
     if rank == 0 and world == 1 and mode == "frames" and not args.no_stream:

@@ -114,7 +114,13 @@ me_status me_full_search(me_ctx* ctx, const uint8_t* ref, const uint8_t* cur,
 
 /* Same search on HBM-resident planes of ctx's first device, enqueued on
  * `stream` (a hipStream_t; NULL = the legacy default stream), asynchronous.
- * d_mv_xy / d_block_cost are device arrays of nblocks entries. */
+ * d_mv_xy / d_block_cost are device arrays of nblocks entries.
+ * Searches of one context are ordered by the library: one enqueued on another
+ * stream than the previous search waits for it on the GPU (an event recorded
+ * on the previous stream at the switch; the host never blocks), so a stream
+ * passed here must stay valid until the context's next search is enqueued.
+ * After the stream has finished, me_device_check() reports a search whose
+ * in-kernel invariant broke (the synchronous entry points check on their own). */
 me_status me_full_search_device(me_ctx* ctx, const uint8_t* d_ref,
                                 const uint8_t* d_cur, int width, int height,
                                 int stride, int block_size, int search_range,
@@ -162,6 +168,34 @@ me_status me_comm_init(me_ctx* ctx, const void* id, int n_ranks, int rank);
  * `stream` (a hipStream_t) after the work already on it; asynchronous. */
 me_status me_gather_device(me_ctx* ctx, const void* d_send, size_t bytes, void* d_recv,
                            void* stream);
+
+/* ME_EDEVICE if a search kernel of this context reported a broken in-kernel
+ * invariant (a bounded wait that expired: the kernel ends instead of hanging
+ * the GPU, and that search's MV field is invalid) since the last check; the
+ * report is cleared.  Call after the searches' streams have finished.
+ * me_full_search, me_find_best_blocks and me_search_pairs check on their own. */
+me_status me_device_check(me_ctx* ctx);
+
+/* ---- captured steps (hipGraph) ----
+ * A per-frame step of device entry points (e.g. a stripe search and its
+ * me_gather_device) recorded once and replayed with one launch: the sharded
+ * step of a small stripe is bound by host enqueue time, not by the GPU.
+ * Counterpart of the reference's per-frame host region (src/gpu/main_mse.cu:202-229).
+ *   me_capture_begin(ctx, s); me_full_search_stripe_device(ctx, ..., s);
+ *   me_gather_device(ctx, ..., s); me_capture_end(ctx, s, &g);
+ *   per frame: me_graph_launch(g, s);
+ * `stream` is a created hipStream_t (not NULL).  Run each search once
+ * uncaptured first: it sizes the context's scratch, and a captured search that
+ * would have to grow it fails with ME_EINVAL.  The captured calls only record;
+ * nothing runs until me_graph_launch, which orders the graph after the
+ * context's previous search like any search.  A graph whose context scratch
+ * was regrown since capture (a larger search ran) is refused (ME_EINVAL).
+ * Destroy graphs before their context. */
+typedef struct me_graph me_graph;
+me_status me_capture_begin(me_ctx* ctx, void* stream);
+me_status me_capture_end(me_ctx* ctx, void* stream, me_graph** graph);
+me_status me_graph_launch(me_graph* graph, void* stream);
+void me_graph_destroy(me_graph* graph);
 
 /* Reference block record, field for field src/common/block.h:6-19 (44 B). */
 typedef struct me_ref_block {

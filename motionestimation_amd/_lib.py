@@ -46,6 +46,12 @@ _SIGS = {
     "me_comm_init": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
     "me_gather_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
                                         ctypes.c_void_p, ctypes.c_void_p]),
+    "me_device_check": (ctypes.c_int, [ctypes.c_void_p]),
+    "me_capture_begin": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "me_capture_end": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.POINTER(ctypes.c_void_p)]),
+    "me_graph_launch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "me_graph_destroy": (None, [ctypes.c_void_p]),
     "me_find_best_blocks": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p] +
                             [ctypes.c_int] * 4 + [ctypes.c_void_p, ctypes.c_int]),
     "me_motion_compensate": (ctypes.c_int, [ctypes.c_void_p, _u8p] + [ctypes.c_int] * 3 +

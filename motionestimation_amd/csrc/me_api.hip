@@ -167,11 +167,12 @@ SearchArgs make_args(const uint8_t* ref, int ref_row0, const uint8_t* cur, int c
   return p;
 }
 
-me_status attach_scratch(me_ctx* c, Dev& d, SearchArgs& p) {
+me_status attach_scratch(me_ctx* c, Dev& d, SearchArgs& p, bool cap) {
   p.sched = d.sched;
   if (p.cost_kind == COST_SSD) {
     const size_t tiles = mfma_merge_tiles(p);
     if (tiles > d.merge_cap) {
+      if (cap) return fail(c, ME_EINVAL, "captured search needs new scratch: run it once uncaptured first");
       (void)hipFree(d.mkeys);
       (void)hipFree(d.mcnt);
       d.mkeys = nullptr;
@@ -189,6 +190,8 @@ me_status attach_scratch(me_ctx* c, Dev& d, SearchArgs& p) {
   p.mcnt = d.mcnt;
   p.merge_tiles = d.merge_cap;
   const size_t need = mfma_ssd_scratch(p);
+  if (need && cap && (need > d.scratch_cap || !d.scratch))
+    return fail(c, ME_EINVAL, "captured search needs new scratch: run it once uncaptured first");
   if (need) {
     me_status s = grow(c, (void**)&d.scratch, &d.scratch_cap, need);
     if (s != ME_OK) return s;
@@ -198,34 +201,58 @@ me_status attach_scratch(me_ctx* c, Dev& d, SearchArgs& p) {
   return ME_OK;
 }
 
-me_status launch_ordered(me_ctx* c, Dev& d, SearchArgs& p, hipStream_t s) {
+bool capturing(hipStream_t s) {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  return s && hipStreamIsCapturing(s, &st) == hipSuccess && st == hipStreamCaptureStatusActive;
+}
+
+me_status order_on(me_ctx* c, Dev& d, hipStream_t s) {
   if (d.searched && d.search_stream != s) {
-    if (d.multi_stream) {
-      HIPCHK(c, hipStreamWaitEvent(s, d.search_ev, 0));
-    } else {
-      // First stream switch of this device: no end event was recorded (one per
-      // search costs ~3 us of GPU time between back-to-back searches, measured
-      // on 1080p and on stripes), so wait for the device once; from now on
-      // every search records one.
-      int prev = d.id;
-      (void)hipGetDevice(&prev);
-      if (prev != d.id) HIPCHK(c, hipSetDevice(d.id));
-      const hipError_t se = hipDeviceSynchronize();
-      if (prev != d.id) (void)hipSetDevice(prev);
-      HIPCHK(c, se);
-      d.multi_stream = true;
-    }
+    // The event is recorded now, on the previous search's stream: it covers
+    // that search (and whatever the caller queued after it there, which only
+    // over-orders).  An event per search instead cost ~3 us of GPU time
+    // between back-to-back searches (1080p 82.3 -> 79.3 us without it), and the
+    // round-2 device-wide synchronisation at the first switch blocked the host
+    // and drained unrelated streams.  The previous stream must still exist
+    // (include/me.h: a stream stays valid until the next search is enqueued).
+    HIPCHK(c, hipEventRecord(d.search_ev, d.search_stream));
+    HIPCHK(c, hipStreamWaitEvent(s, d.search_ev, 0));
+  }
+  d.search_stream = s;
+  d.searched = true;
+  return ME_OK;
+}
+
+me_status launch_ordered(me_ctx* c, Dev& d, SearchArgs& p, hipStream_t s) {
+  // Captured launches run only when their graph does (me_graph_launch orders
+  // it): no ordering and no state change at capture time.
+  const bool cap = capturing(s);
+  if (!cap) {
+    me_status st = order_on(c, d, s);
+    if (st != ME_OK) return st;
   }
   const hipError_t e = launch_search(p, s, nullptr);
   if (e != hipSuccess) {
-    (void)hipMemsetAsync(d.sched, 0, 64, s);
-    if (d.mkeys) (void)hipMemsetAsync(d.mkeys, 0xFF, d.merge_cap * 16 * 8, s);
-    if (d.mcnt) (void)hipMemsetAsync(d.mcnt, 0, d.merge_cap * 4, s);
+    if (!cap) {
+      (void)hipMemsetAsync(d.sched, 0, 64, s);
+      if (d.mkeys) (void)hipMemsetAsync(d.mkeys, 0xFF, d.merge_cap * 16 * 8, s);
+      if (d.mcnt) (void)hipMemsetAsync(d.mcnt, 0, d.merge_cap * 4, s);
+    }
     return fail(c, ME_EDEVICE, "search launch: %s", hipGetErrorString(e));
   }
-  if (d.multi_stream) HIPCHK(c, hipEventRecord(d.search_ev, s));
-  d.search_stream = s;
-  d.searched = true;
+  return ME_OK;
+}
+
+me_status device_status(me_ctx* c, Dev& d, hipStream_t s) {
+  uint32_t w = 0;
+  HIPCHK(c, hipMemcpyAsync(&w, d.sched + SCHED_ERR, 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipStreamSynchronize(s));
+  if (w) {
+    HIPCHK(c, hipMemsetAsync(d.sched + SCHED_ERR, 0, 4, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    return fail(c, ME_EDEVICE, "device %d: a search kernel's bounded wait expired (code %u): "
+                "the MV field of that search is invalid", d.id, w);
+  }
   return ME_OK;
 }
 
@@ -239,23 +266,6 @@ using me::check_args;
 using me::make_args;
 using me::attach_scratch;
 using me::launch_ordered;
-
-uint64_t row_candidates(int width, int height, int blk, int range, int by) {
-  const int nbx = (width + blk - 1) / blk;
-  const int tly = by * blk;
-  const int h = height - tly < blk ? height - tly : blk;
-  const int dymin = -range > -tly ? -range : -tly;
-  const int dymax = range < height - h - tly ? range : height - h - tly;
-  uint64_t ny = (uint64_t)(dymax - dymin + 1), total = 0;
-  for (int bx = 0; bx < nbx; bx++) {
-    const int tlx = bx * blk;
-    const int w = width - tlx < blk ? width - tlx : blk;
-    const int dxmin = -range > -tlx ? -range : -tlx;
-    const int dxmax = range < width - w - tlx ? range : width - w - tlx;
-    total += (uint64_t)(dxmax - dxmin + 1) * ny;
-  }
-  return total;
-}
 
 me_status ensure_comms(me_ctx* c) {
   if (c->comms || !c->distinct || c->devs.size() < 2) return ME_OK;
@@ -359,7 +369,7 @@ me_status multi_search(me_ctx* c, const uint8_t* ref, const uint8_t* cur, int wi
   }
   for (int i = 0; i < n; i++) {
     HIPCHK(c, hipSetDevice(c->devs[i].id));
-    HIPCHK(c, hipStreamSynchronize(c->devs[i].stream));
+    if ((s = me::device_status(c, c->devs[i], c->devs[i].stream)) != ME_OK) return s;
   }
   HIPCHK(c, hipSetDevice(root.id));
   std::vector<uint8_t> host(rec_bytes * n);
@@ -397,51 +407,6 @@ const char* me_version(void) { return "me_hip 1 gfx950"; }
 
 void me_set_kernel_path(me_path path) {
   me::set_kernel_path_code(path == ME_PATH_VALU ? 1 : path == ME_PATH_MFMA_TILES ? 2 : 0);
-}
-
-int me_num_blocks(int width, int height, int blk) {
-  if (width <= 0 || height <= 0 || blk <= 0) return 0;
-  return ((width + blk - 1) / blk) * ((height + blk - 1) / blk);
-}
-
-uint64_t me_candidate_count(int width, int height, int blk, int range) {
-  if (width <= 0 || height <= 0 || blk <= 0 || range < 0) return 0;
-  uint64_t t = 0;
-  const int nby = (height + blk - 1) / blk;
-  for (int by = 0; by < nby; by++) t += row_candidates(width, height, blk, range, by);
-  return t;
-}
-
-me_status me_plan_stripes(int width, int height, int blk, int range, int n, int* bounds) {
-  if (!bounds || n < 1 || width <= 0 || height <= 0 || blk <= 0 || range < 0) return ME_EINVAL;
-  const int nby = (height + blk - 1) / blk;
-  // Row cost (include/me.h): nbx * (3 (2S + 1) + ny) -- an exact-candidate
-  // balance gave the 4K +-64 edge stripes 18 block rows against 16-17 inside,
-  // and 2,160 two-block tiles take three rounds of the chip's 1,024 workgroup
-  // slots where 2,040 take two (8-way 4K edge stripe 0.200 vs 0.153 ms,
-  // profiles/r02i_stripe_4k.jsonl).
-  std::vector<uint64_t> cum(nby + 1, 0);
-  const uint64_t nbx = (uint64_t)((width + blk - 1) / blk);
-  for (int by = 0; by < nby; by++) {
-    const int tly = by * blk;
-    const int h = height - tly < blk ? height - tly : blk;
-    const int dymin = -range > -tly ? -range : -tly;
-    const int dymax = range < height - h - tly ? range : height - h - tly;
-    const uint64_t ny = (uint64_t)(dymax - dymin + 1);
-    cum[by + 1] = cum[by] + nbx * (3 * (uint64_t)(2 * range + 1) + ny);
-  }
-  bounds[0] = 0;
-  int r = 0;
-  for (int i = 1; i < n; i++) {
-    const double target = (double)cum[nby] * i / n;
-    while (r < nby && (double)cum[r + 1] <= target) r++;
-    // pick the nearer boundary
-    if (r < nby && target - (double)cum[r] > (double)cum[r + 1] - target) r++;
-    if (r < bounds[i - 1]) r = bounds[i - 1];
-    bounds[i] = r;
-  }
-  bounds[n] = nby;
-  return ME_OK;
 }
 
 me_status me_create(me_ctx** out, const int* device_ids, int n) {
@@ -531,6 +496,82 @@ me_status me_gather_device(me_ctx* c, const void* d_send, size_t bytes, void* d_
   return ME_OK;
 }
 
+me_status me_device_check(me_ctx* c) {
+  if (!c) return ME_EINVAL;
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  me_status s = ME_OK;
+  for (Dev& d : c->devs) {
+    uint32_t w = 0;
+    if (hipSetDevice(d.id) != hipSuccess ||
+        hipMemcpy(&w, d.sched + me::SCHED_ERR, 4, hipMemcpyDeviceToHost) != hipSuccess) {
+      s = fail(c, ME_EDEVICE, "device %d: reading the invariant word failed", d.id);
+      break;
+    }
+    if (w) {
+      (void)hipMemset(d.sched + me::SCHED_ERR, 0, 4);
+      s = fail(c, ME_EDEVICE, "device %d: a search kernel's bounded wait expired (code %u): "
+               "the MV field of that search is invalid", d.id, w);
+      break;
+    }
+  }
+  (void)hipSetDevice(prev);
+  return s;
+}
+
+// A captured step: the graph plus what its searches point into.
+struct me_graph {
+  me_ctx* ctx;
+  hipGraphExec_t exec;
+  const void *sched, *scratch, *mkeys, *mcnt;
+};
+
+me_status me_capture_begin(me_ctx* c, void* stream) {
+  if (!c) return ME_EINVAL;
+  if (!stream) return fail(c, ME_EINVAL, "capture needs a created stream, not the NULL stream");
+  c->err[0] = 0;
+  HIPCHK(c, hipStreamBeginCapture((hipStream_t)stream, hipStreamCaptureModeRelaxed));
+  return ME_OK;
+}
+
+me_status me_capture_end(me_ctx* c, void* stream, me_graph** out) {
+  if (!c) return ME_EINVAL;
+  if (!out) return fail(c, ME_EINVAL, "null graph pointer");
+  *out = nullptr;
+  hipGraph_t g = nullptr;
+  HIPCHK(c, hipStreamEndCapture((hipStream_t)stream, &g));
+  hipGraphExec_t ex = nullptr;
+  const hipError_t e = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(g);
+  HIPCHK(c, e);
+  const Dev& d = c->devs[0];
+  me_graph* gr = new (std::nothrow) me_graph{c, ex, d.sched, d.scratch, d.mkeys, d.mcnt};
+  if (!gr) {
+    (void)hipGraphExecDestroy(ex);
+    return fail(c, ME_ENOMEM, "graph");
+  }
+  *out = gr;
+  return ME_OK;
+}
+
+me_status me_graph_launch(me_graph* g, void* stream) {
+  if (!g) return ME_EINVAL;
+  me_ctx* c = g->ctx;
+  Dev& d = c->devs[0];
+  if (d.sched != g->sched || d.scratch != g->scratch || d.mkeys != g->mkeys || d.mcnt != g->mcnt)
+    return fail(c, ME_EINVAL, "the context's search scratch was regrown after capture: capture again");
+  me_status s = me::order_on(c, d, (hipStream_t)stream);
+  if (s != ME_OK) return s;
+  HIPCHK(c, hipGraphLaunch(g->exec, (hipStream_t)stream));
+  return ME_OK;
+}
+
+void me_graph_destroy(me_graph* g) {
+  if (!g) return;
+  (void)hipGraphExecDestroy(g->exec);
+  delete g;
+}
+
 void me_destroy(me_ctx* c) {
   if (!c) return;
   if (c->rank_comm) ncclCommDestroy(c->rank_comm);
@@ -584,8 +625,7 @@ me_status me_full_search(me_ctx* c, const uint8_t* ref, const uint8_t* cur, int 
   HIPCHK(c, hipMemcpyAsync(mv_xy, dmv, nb * 4, hipMemcpyDeviceToHost, d.stream));
   if (block_cost)
     HIPCHK(c, hipMemcpyAsync(block_cost, dcost, nb * 4, hipMemcpyDeviceToHost, d.stream));
-  HIPCHK(c, hipStreamSynchronize(d.stream));
-  return ME_OK;
+  return me::device_status(c, d, d.stream);
 }
 
 me_status me_full_search_stripe_device(me_ctx* c, const uint8_t* d_ref, int ref_row0,
@@ -603,7 +643,8 @@ me_status me_full_search_stripe_device(me_ctx* c, const uint8_t* d_ref, int ref_
   c->err[0] = 0;
   me::SearchArgs p = make_args(d_ref, ref_row0, d_cur, cur_row0, width, height, stride, blk,
                                range, cost, r0, r1, d_mv, d_cost);
-  if ((s = attach_scratch(c, c->devs[0], p)) != ME_OK) return s;
+  const bool cap = me::capturing((hipStream_t)stream);
+  if ((s = attach_scratch(c, c->devs[0], p, cap)) != ME_OK) return s;
   return launch_ordered(c, c->devs[0], p, (hipStream_t)stream);
 }
 
@@ -625,8 +666,13 @@ me_status me_find_best_blocks(me_ctx* c, const int* ref_frame, const int* cur_fr
   const size_t plane = (size_t)width * height;
   std::vector<uint8_t> r8(plane), c8(plane);
   for (size_t i = 0; i < plane; i++) {  // utils.c:49-53 widened u8 -> int; narrow back
-    r8[i] = (uint8_t)ref_frame[i];
-    c8[i] = (uint8_t)cur_frame[i];
+    const int rv = ref_frame[i], cv = cur_frame[i];
+    // the planes came from 8-bit files: anything else would be searched as
+    // its low byte and give a field the reference would not
+    if ((unsigned)rv > 255u || (unsigned)cv > 255u)
+      return fail(c, ME_EINVAL, "pixel %zu (%d, %d) outside [0, 255]", i, rv, cv);
+    r8[i] = (uint8_t)rv;
+    c8[i] = (uint8_t)cv;
   }
   std::vector<int16_t> mv((size_t)nb * 2);
   s = me_full_search(c, r8.data(), c8.data(), width, height, width, blk, range, ME_COST_SSD,

@@ -37,12 +37,13 @@ struct Dev {
   size_t merge_cap = 0;                 //   (tiles)
   // The counters, merge keys and scratch above serve one search at a time:
   // a search issued on another stream than the previous one first waits for
-  // it (launch_ordered): a device-wide wait at the first switch, then
-  // search_ev, recorded after every search once the device has seen two streams.
+  // it (launch_ordered): search_ev is recorded on the previous search's stream
+  // at the switch and the new stream waits for it (no host block, no event
+  // per search).  Searches captured into a graph (me_capture_begin) are not
+  // executed at capture: me_graph_launch orders the graph the same way.
   hipEvent_t search_ev = nullptr;
   hipStream_t search_stream = nullptr;
   bool searched = false;
-  bool multi_stream = false;
   // Frame-pair pipeline (me_stream.hip), kept across calls.
   std::vector<uint8_t*> slots;        // device frames, slot_bytes each
   std::vector<hipEvent_t> slot_ready; // upload of the slot's frame done (copy stream)
@@ -70,7 +71,9 @@ SearchArgs make_args(const uint8_t* ref, int ref_row0, const uint8_t* cur, int c
 // Point p at d's search scratch, growing it to what p's search needs.  A
 // device's scratch serves one search at a time: launch searches that use it
 // with launch_ordered.
-me_status attach_scratch(me_ctx* c, Dev& d, SearchArgs& p);
+// cap: the launch is being captured (me_capture_begin): growing the scratch
+// then fails with ME_EINVAL (a graph must not hold buffers a later search frees).
+me_status attach_scratch(me_ctx* c, Dev& d, SearchArgs& p, bool cap = false);
 
 // Launch p (scratch attached) on stream s after every earlier search of d:
 // a search arriving on a different stream than the previous one first waits
@@ -78,6 +81,18 @@ me_status attach_scratch(me_ctx* c, Dev& d, SearchArgs& p);
 // tile counters and merge buffers (a partly run kernel may have left them
 // dirty) before returning ME_EDEVICE.
 me_status launch_ordered(me_ctx* c, Dev& d, SearchArgs& p, hipStream_t s);
+
+// Order stream s after the device's previous search (a stream switch) and
+// make s the device's search stream; `launch` then enqueues on s.
+me_status order_on(me_ctx* c, Dev& d, hipStream_t s);
+
+// True while s is being captured into a graph (me_capture_begin).
+bool capturing(hipStream_t s);
+
+// Read and clear the device's in-kernel invariant word (sched[SCHED_ERR])
+// after the work on stream s: ME_EDEVICE if a kernel reported a broken
+// invariant (a bounded wait that expired), ME_OK otherwise.  Synchronises s.
+me_status device_status(me_ctx* c, Dev& d, hipStream_t s);
 
 // Pinned host ranges handed out by me_host_alloc (the pair pipeline DMAs
 // straight from them instead of staging).

@@ -7,6 +7,7 @@
 // The MV-field file is this build's own format (the reference never writes
 // its MVs): a 32-byte header and, per pair, the raster-order MV records and
 // optional costs, little-endian.
+#include <stdint.h>
 #include <stdio.h>
 #include <string.h>
 
@@ -38,10 +39,21 @@ bool bad_geometry(int width, int height, me_yuv_layout layout) {
   return width <= 0 || height <= 0 || (layout != ME_YUV_LUMA && layout != ME_YUV_I420);
 }
 
+// Bytes one pair occupies in the file (indices, MV records, costs).
+int64_t pair_bytes(const me_mv_header& h) {
+  const int64_t nb = me_num_blocks(h.width, h.height, h.block_size);
+  return 8 + nb * ((h.flags & 1) ? 8 : 4);
+}
+
 bool valid_header(const me_mv_header& h) {
-  return memcmp(h.magic, "MEMV", 4) == 0 && h.version == 1 && h.width > 0 && h.height > 0 &&
-         h.block_size > 0 && h.block_size <= ME_MAX_BLOCK && h.search_range >= 0 &&
-         (h.cost == ME_COST_SSD || h.cost == ME_COST_SAD || h.cost == ME_COST_SSIM);
+  if (!(memcmp(h.magic, "MEMV", 4) == 0 && h.version == 1 && h.flags <= 1 && h.width > 0 &&
+        h.height > 0 && h.block_size > 0 && h.block_size <= ME_MAX_BLOCK &&
+        h.search_range >= 0 &&
+        (h.cost == ME_COST_SSD || h.cost == ME_COST_SAD || h.cost == ME_COST_SSIM)))
+    return false;
+  // the block count fits an int and the whole file an int64 (hostile headers)
+  if (me_num_blocks(h.width, h.height, h.block_size) <= 0) return false;
+  return (int64_t)h.n_pairs <= (INT64_MAX - 32) / pair_bytes(h);
 }
 
 }  // namespace
@@ -63,7 +75,9 @@ me_status me_yuv_read_luma(const char* path, int width, int height, me_yuv_layou
     return ME_EINVAL;
   File f(fopen(path, "rb"));
   if (!f.f) return ME_EIO;
-  const int64_t off = frame_bytes(width, height, layout) * frame_index;
+  const int64_t fb = frame_bytes(width, height, layout);
+  if ((int64_t)frame_index > (INT64_MAX - fb) / fb) return ME_EIO;  // past any file
+  const int64_t off = fb * frame_index;
   if (fseeko(f.f, (off_t)off, SEEK_SET) != 0) return ME_EIO;
   if (dst_stride == width)
     return fread(dst, (size_t)width * height, 1, f.f) == 1 ? ME_OK : ME_EIO;
@@ -134,7 +148,7 @@ me_status me_mv_read(const char* path, me_mv_header* hdr, int* pairs, int16_t* m
   const bool has_cost = h.flags & 1;
   // Size check before any read: a truncated file is an error, not a short result.
   const int64_t size = file_size(f.f);
-  const int64_t need = (int64_t)sizeof h + (int64_t)h.n_pairs * (8 + nb * (has_cost ? 8 : 4));
+  const int64_t need = (int64_t)sizeof h + (int64_t)h.n_pairs * pair_bytes(h);  // valid_header: no overflow
   if (size != need) return ME_EIO;
   if (fseeko(f.f, (off_t)sizeof h, SEEK_SET) != 0) return ME_EIO;
   for (uint32_t n = 0; n < h.n_pairs; n++) {

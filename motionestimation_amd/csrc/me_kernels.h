@@ -11,6 +11,9 @@ enum { COST_SSD = 0, COST_SAD = 1, COST_SSIM = 2 };
 constexpr int GENERIC_THREADS = 256;
 constexpr int GENERIC_LDS_BUDGET = 60 * 1024;
 constexpr int QSAD_LDS_BUDGET = 40 * 1024;  // 4 workgroups per CU (160 KB LDS)
+// sched[SCHED_ERR]: a kernel whose bounded wait expired sets it (the host
+// reads and clears it: device_status, me_device_check).  sched holds 16 u32.
+constexpr int SCHED_ERR = 15;
 
 // One search launch: block rows [block_row_begin, block_row_end) of a
 // width x height frame.  ref / cur point at frame rows ref_row0 / cur_row0.
@@ -28,7 +31,8 @@ struct SearchArgs {
   uint32_t* cost;
   uint32_t ref_bytes;  // readable bytes from ref (buffer range check), and from cur
   uint32_t cur_bytes;
-  uint32_t* sched;     // 9 zeroed u32 (8 XCD-group tile counters + arrivals) or null
+  uint32_t* sched;     // 16 u32: [0, 9) zeroed tile counters + arrivals (8 XCD groups),
+                       // [SCHED_ERR] the invariant word; or null
   uint8_t* scratch;    // device scratch of the MFMA SSD path (mfma_ssd_scratch bytes) or null
   size_t scratch_bytes;
   // MFMA SSD cross-workgroup merge (self-resetting): 16 keys (~0) per tile and
@@ -93,6 +97,9 @@ size_t mfma_ssd_scratch(const SearchArgs& p);  // 0: path not applicable
 bool mfma_disabled();
 
 hipError_t launch_search(const SearchArgs& p, hipStream_t stream, int* used_fast);
+// Raise fn's dynamic-LDS limit to lds (> 64 KB) on the current device, once
+// per (kernel, device, larger size): process-wide cache, thread-safe.
+hipError_t lds_attr(const void* fn, int lds);
 hipError_t launch_generic(const SearchArgs& p, int bx0, int nbx_range, int row0, int nrows,
                           hipStream_t stream);
 bool plan_fast(const SearchArgs& p, QsadGeom* g, int* k_out);

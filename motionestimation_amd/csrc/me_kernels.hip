@@ -8,13 +8,21 @@
 // with an unsigned min: the smallest key is the smallest cost and, among equal
 // costs, the smallest (dy, dx) -- the reference's raster-first choice.
 //
-// Two kernels:
-//   me_qsad_kernel<B, K>   SAD, B in {8, 16}, full-width blocks.  One workgroup
-//                          per TB blocks of one block row; the union search
-//                          window of those blocks is staged once in LDS; each
-//                          lane owns 4 horizontal x K vertical candidates of one
-//                          block and walks the window rows, 16 |a-b| per
-//                          v_qsad_pk_u16_u8 with the cur block held in VGPRs.
+// Kernels (the matrix-core SSD kernels are in me_mfma.hip, SSIM in me_ssim.hip):
+//   me_fast_kernel<COST, B, K, PC>
+//                          SAD (qsad) or SSD (dot4), B in {8, 16}, full-width
+//                          blocks.  Persistent and double-buffered: an item is
+//                          (tile of TB blocks of one block row, pass of dy
+//                          chunks); the union search window of the tile is
+//                          staged once in LDS by LDS DMA; each SAD lane owns 4
+//                          horizontal x K vertical candidates of one block and
+//                          walks the window rows, 16 |a-b| per v_qsad_pk_u16_u8
+//                          with the cur block held in VGPRs.
+//   me_flow_kernel<B, K, PC>
+//                          SAD, 16x16, S = 32 on frames with >= 2 tiles per CU
+//                          (the 1080p headline): one 1,024-thread workgroup
+//                          per CU, a ring of LDS slots, waves pulling 64-lane
+//                          wave-tasks from one LDS counter (no item barriers).
 //   me_generic_kernel      any B <= 64, any S, SSD or SAD, partial blocks; one
 //                          workgroup per block, one candidate per lane.  SSD on
 //                          blocks with w*h > 256 replays the reference's float
@@ -25,7 +33,9 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <mutex>
 #include <type_traits>
+#include <vector>
 
 #include "me_kernels.h"
 #include "me_tuning.h"
@@ -933,8 +943,9 @@ __global__ __launch_bounds__(1024) void me_flow_kernel(SearchArgs p, QsadGeom g)
     if (kc >= nitems) break;
     const int slot = kc % NB;
     // Bounded wait (the ordering argument above says it ends; the bound keeps a
-    // broken invariant from hanging the GPU: the search would then be wrong,
-    // which every parity test catches, instead of never finishing).
+    // broken invariant from hanging the GPU).  An expired wait is reported:
+    // sched[SCHED_ERR] is set, and the host turns it into ME_EDEVICE
+    // (device_status after the synchronous entry points, me_device_check).
     int spins = 0;
 #ifdef ME_STAMPS
     const unsigned long long st_w0 = __builtin_amdgcn_s_memtime();
@@ -943,7 +954,11 @@ __global__ __launch_bounds__(1024) void me_flow_kernel(SearchArgs p, QsadGeom g)
                (uint32_t)kc + 1u &&
            ++spins < (1 << 20))
       __builtin_amdgcn_s_sleep(2);
-    if (spins >= (1 << 20)) break;
+    if (spins >= (1 << 20)) {
+      if (lane == 0 && p.sched)
+        __hip_atomic_store(p.sched + SCHED_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
 #ifdef ME_STAMPS
     {
       const unsigned long long now = __builtin_amdgcn_s_memtime();
@@ -1367,23 +1382,69 @@ bool plan_flow(const SearchArgs& p, QsadGeom* g) {
   return q.lds <= 160 * 1024;
 }
 
+// Per-kernel launch facts, computed once per (kernel, device[, shape]) and
+// shared by every host thread (a mutex-protected list: the per-device threads
+// of multi_search and me_search_pairs plan and launch concurrently).  Setting
+// the dynamic-LDS attribute and querying occupancy on every launch cost host
+// time on the small-stripe step, which is host-bound.
+namespace {
+struct LaunchFact {
+  const void* fn;
+  int dev, threads, lds, value;  // threads == 0: the LDS attribute entry (value = max set)
+};
+std::mutex g_fact_mu;
+std::vector<LaunchFact> g_facts;
+
+int current_device() {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  return dev;
+}
+}  // namespace
+
+hipError_t lds_attr(const void* fn, int lds) {
+  if (lds <= 64 * 1024) return hipSuccess;
+  const int dev = current_device();
+  std::lock_guard<std::mutex> lk(g_fact_mu);
+  for (LaunchFact& f : g_facts)
+    if (f.fn == fn && f.dev == dev && f.threads == 0) {
+      if (f.value >= lds) return hipSuccess;
+      const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      if (e == hipSuccess) f.value = lds;
+      return e;
+    }
+  const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  if (e == hipSuccess) g_facts.push_back({fn, dev, 0, 0, lds});
+  return e;
+}
+
 // Resident workgroups per CU for this kernel / block / LDS.
 static int resident_wgs(const void* fn, int threads, int lds) {
+  const int dev = current_device();
+  {
+    std::lock_guard<std::mutex> lk(g_fact_mu);
+    for (const LaunchFact& f : g_facts)
+      if (f.fn == fn && f.dev == dev && f.threads == threads && f.lds == lds) return f.value;
+  }
   int n = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, threads, lds) != hipSuccess || n < 1)
     n = 1;
+  std::lock_guard<std::mutex> lk(g_fact_mu);
+  g_facts.push_back({fn, dev, threads, lds, n});
   return n;
 }
 
+// CUs of the device (every device of a context is the same part): a C++11
+// function-local static, initialised once and thread-safely (multi_search and
+// me_search_pairs call the planners from one host thread per device).
 static int cu_count() {
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
+  static const int cus = []() {
+    int dev = 0, n = 0;
     (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        cus < 1)
-      cus = 256;
-  }
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 1)
+      n = 256;
+    return n;
+  }();
   return cus;
 }
 
@@ -1399,13 +1460,9 @@ hipError_t launch_fast(const SearchArgs& p, QsadGeom g, int K, int row0, int nro
 #define ME_FAST_CASE_P(CC, BB, KK, PP)                                                     \
   if (p.cost_kind == CC && p.blk == BB && K == KK && (PP == 0 || g.pitch == PP)) {         \
     const void* fn = (const void*)me_fast_kernel<CC, BB, KK, PP>;                         \
-    if (g.lds > 64 * 1024) {                                                               \
-      hipError_t e_ = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, g.lds); \
-      if (e_ != hipSuccess) return e_;                                                     \
-    }                                                                                      \
-    thread_local int res_lds = -1, res_n = 1;                                              \
-    if (res_lds != g.lds) { res_n = resident_wgs(fn, g.threads, g.lds); res_lds = g.lds; } \
-    const int res = res_n;                                                                 \
+    const hipError_t e_ = lds_attr(fn, g.lds);                                             \
+    if (e_ != hipSuccess) return e_;                                                       \
+    const int res = resident_wgs(fn, g.threads, g.lds);                                    \
     const int nwg = ntiles < res * cu_count() ? ntiles : res * cu_count();                 \
     hipLaunchKernelGGL((me_fast_kernel<CC, BB, KK, PP>), dim3((unsigned)nwg), block, g.lds, stream, p, g); \
     return hipGetLastError();                                                              \
@@ -1425,8 +1482,9 @@ hipError_t launch_fast(const SearchArgs& p, QsadGeom g, int K, int row0, int nro
   return hipErrorInvalidValue;
 }
 
-// Plans depend only on the search shape: cache them (per host thread) so a
-// steady stream of same-shape searches pays the planner once.
+// Plans depend only on the search shape: cache them (process-wide, under a
+// mutex: the per-device threads of multi_search and me_search_pairs share
+// them) so a steady stream of same-shape searches pays the planner once.
 struct PlanKey {
   int width, height, stride, blk, range, cost, rows, aligned;  // aligned: 1 (4 B) | 2 (16 B)
   bool operator==(const PlanKey& o) const {
@@ -1443,13 +1501,15 @@ struct PlanEntry {
 
 static bool cached_plan(const SearchArgs& p, QsadGeom* g, int* K) {
   constexpr int N = 8;
-  thread_local PlanEntry cache[N];
-  thread_local int used = 0, next = 0;
+  static PlanEntry cache[N];
+  static int used = 0, next = 0;
+  static std::mutex mu;
   const int aligned =
       ((p.stride % 4 == 0) && ((uintptr_t)p.ref % 4 == 0) && ((uintptr_t)p.cur % 4 == 0)) |
       (((p.stride % 16 == 0) && ((uintptr_t)p.ref % 16 == 0)) << 1);
   const PlanKey key{p.width, p.height, p.stride, p.blk, p.range, p.cost_kind,
                     p.block_row_end - p.block_row_begin, aligned};
+  std::lock_guard<std::mutex> lk(mu);
   for (int i = 0; i < used; i++)
     if (cache[i].key == key) {
       *g = cache[i].g;
@@ -1469,12 +1529,14 @@ static bool cached_plan(const SearchArgs& p, QsadGeom* g, int* K) {
 
 static bool cached_flow_plan(const SearchArgs& p, QsadGeom* g) {
   constexpr int N = 8;
-  thread_local PlanEntry cache[N];
-  thread_local int used = 0, next = 0;
+  static PlanEntry cache[N];
+  static int used = 0, next = 0;
+  static std::mutex mu;
   const int aligned = ((p.stride % 16 == 0) && ((uintptr_t)p.ref % 16 == 0) &&
                        ((uintptr_t)p.cur % 16 == 0)) ? 3 : 0;
   const PlanKey key{p.width, p.height, p.stride, p.blk, p.range, p.cost_kind,
                     p.block_row_end - p.block_row_begin, aligned};
+  std::lock_guard<std::mutex> lk(mu);
   for (int i = 0; i < used; i++)
     if (cache[i].key == key) {
       *g = cache[i].g;
@@ -1501,7 +1563,7 @@ static hipError_t launch_flow(const SearchArgs& p, QsadGeom g, int row0, int nro
   // the ds_read2 offsets); any other pitch takes the runtime-pitch body
   const void* fn = g.pitch == 144 ? (const void*)me_flow_kernel<16, FLOW_K, 144>
                                   : (const void*)me_flow_kernel<16, FLOW_K, 0>;
-  hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, g.lds);
+  hipError_t e = lds_attr(fn, g.lds);
   if (e != hipSuccess) return e;
   const int nwg = ntiles < cu_count() ? ntiles : cu_count();
   if (g.pitch == 144)

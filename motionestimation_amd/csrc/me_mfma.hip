@@ -1410,11 +1410,8 @@ hipError_t launch_mfma_ssd(const SearchArgs& p, const MfmaGeom& g, hipStream_t s
   if (e != hipSuccess) return e;
   if (p.blk == 8) {
     const dim3 grid8((unsigned)(g.tiles_x * g.tiles_y * g.ngx));
-    if (g.lds > 64 * 1024) {
-      e = hipFuncSetAttribute((const void*)me_mfma_ssd8_kernel<ME_SSD8_KM>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, g.lds);
-      if (e != hipSuccess) return e;
-    }
+    e = lds_attr((const void*)me_mfma_ssd8_kernel<ME_SSD8_KM>, g.lds);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(me_mfma_ssd8_kernel<ME_SSD8_KM>, grid8, dim3(256), g.lds, stream, p, g);
     return hipGetLastError();
   }
@@ -1430,11 +1427,8 @@ hipError_t launch_mfma_ssd(const SearchArgs& p, const MfmaGeom& g, hipStream_t s
   const dim3 grid((unsigned)(g.tiles_x * g.tiles_y * wpt));
 #define ME_MFMA_CASE(NG, KK)                                                              \
   if (g.ngxw == NG && g.km == KK) {                                                       \
-    if (g.lds > 64 * 1024) {                                                              \
-      e = hipFuncSetAttribute((const void*)me_mfma_ssd16_kernel<NG, KK>,                  \
-                              hipFuncAttributeMaxDynamicSharedMemorySize, g.lds);         \
-      if (e != hipSuccess) return e;                                                      \
-    }                                                                                     \
+    e = lds_attr((const void*)me_mfma_ssd16_kernel<NG, KK>, g.lds);                        \
+    if (e != hipSuccess) return e;                                                        \
     hipLaunchKernelGGL((me_mfma_ssd16_kernel<NG, KK>), grid, dim3(256 * NG), g.lds, stream, p, g); \
     return hipGetLastError();                                                             \
   }

@@ -247,8 +247,7 @@ me_status run_pairs(me_ctx* c, Dev& d, const Job& j, int p0, int p1) {
   if (j.block_cost)
     HIPCHK(c, hipMemcpyAsync(j.block_cost + nb * p0, out_cost, np * nb * 4,
                              hipMemcpyDeviceToHost, d.stream));
-  HIPCHK(c, hipStreamSynchronize(d.stream));
-  return ME_OK;
+  return me::device_status(c, d, d.stream);
 }
 
 }  // namespace

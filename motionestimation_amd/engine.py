@@ -35,7 +35,10 @@ def candidate_count(width: int, height: int, blk: int, span: int) -> int:
 
 
 def plan_stripes(width: int, height: int, blk: int, span: int, shards: int) -> list:
-    """Block-row boundaries [b0=0, ..., b_n=nby] balancing exact candidate counts."""
+    """Block-row boundaries [b0=0, ..., b_n=nby] balancing the kernels' cost
+    model (me_plan_stripes, include/me.h): a block row costs
+    nbx * (3 (2S+1) + ny), so a clipped edge row is discounted by a quarter of
+    its candidate deficit, not all of it."""
     out = (ctypes.c_int * (shards + 1))()
     check(_lib.lib().me_plan_stripes(width, height, blk, span, shards, out))
     return list(out)
@@ -78,6 +81,8 @@ class Engine:
 
     def close(self) -> None:
         if getattr(self, "_h", None):
+            for g in getattr(self, "_graphs", ()):
+                g.close()
             _lib.lib().me_destroy(self._h)
             self._h = None
 
@@ -205,6 +210,30 @@ class Engine:
             recv_t.data_ptr() if recv_t is not None else None, st), self._h)
 
 
+    def device_check(self) -> None:
+        """Raise MEError (ME_EDEVICE) if a search kernel reported a broken
+        in-kernel invariant since the last check (call after synchronising)."""
+        check(_lib.lib().me_device_check(self._h), self._h)
+
+    # ---- captured steps: one graph launch per frame ----
+    def capture(self, stream, enqueue) -> "Graph":
+        """Record what enqueue() puts on `stream` (device entry points of this
+        context, e.g. a stripe search and its gather) as one graph.  Run the
+        searches once uncaptured first (they size the context's scratch)."""
+        L = _lib.lib()
+        check(L.me_capture_begin(self._h, stream), self._h)
+        try:
+            enqueue()
+        finally:
+            g = ctypes.c_void_p()
+            st = L.me_capture_end(self._h, stream, ctypes.byref(g))
+        check(st, self._h)
+        gr = Graph(self, g)
+        if not hasattr(self, "_graphs"):
+            self._graphs = []
+        self._graphs.append(gr)  # destroyed before the context (include/me.h)
+        return gr
+
     # ---- prepared calls: arguments marshalled once per buffer set ----
     # A sharded step on a small stripe is bound by host time (an 8-way 1080p
     # stripe searches in 15-18 us), so the per-frame calls skip the wrapper's
@@ -238,6 +267,40 @@ class Engine:
             if s:
                 check(s, h)
         return run
+
+
+class Graph:
+    """A captured step (me_capture_begin/end); launch() replays it on a stream."""
+
+    def __init__(self, eng: Engine, handle):
+        self._eng, self._h = eng, handle
+        self._launch = _lib.lib().me_graph_launch
+
+    def launch(self, stream) -> None:
+        s = self._launch(self._h, stream)
+        if s:
+            check(s, self._eng._h)
+
+    def prepared(self, stream):
+        """Zero-argument callable launching the graph on `stream`."""
+        fn, h, ctx = self._launch, self._h, self._eng._h
+
+        def run():
+            s = fn(h, stream)
+            if s:
+                check(s, ctx)
+        return run
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            _lib.lib().me_graph_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class _Pinned:

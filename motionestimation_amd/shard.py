@@ -1,7 +1,8 @@
 """Row-stripe sharding of one frame search across ranks (one process per GPU).
 
 SURVEY §8e: every macroblock is independent, so rank r searches block rows
-[b_r, b_{r+1}) (balanced by exact candidate count, ``me_plan_stripes``) from
+[b_r, b_{r+1}) (balanced by the kernels' cost model ``me_plan_stripes``:
+nbx * (3 (2S+1) + ny) per block row, include/me.h) from
 the planes it holds: cur rows [b_r*B, b_{r+1}*B) and ref rows with an S-row
 halo.  The only exchange is one gather of the per-stripe MV records to rank 0
 (RCCL over xGMI with the ``nccl`` backend, gloo on CPU in the tests).

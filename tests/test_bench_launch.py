@@ -1,0 +1,63 @@
+"""bench.py's rank setup, on the CPU: `--gpus N` never degrades to a one-rank
+line.  Without a launcher bench.py starts its own N ranks (launch_ranks); a
+request for more RCCL ranks than visible GPUs, or a --gpus that disagrees with
+the launcher's WORLD_SIZE, exits non-zero with nothing on stdout.  The spawn
+itself is exercised on the GPU box (tests/test_gpu_multi.py)."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(REPO, "bench.py")
+
+
+def _gpus():
+    import torch
+    return torch.cuda.device_count()
+
+
+def _run(args, env_extra=None):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, BENCH, *args, "--no-cpu"], capture_output=True,
+                          text=True, timeout=120, env=env)
+
+
+@pytest.mark.skipif("_gpus() >= 2", reason="the box has enough GPUs: the spawn would run")
+def test_more_rccl_ranks_than_gpus_is_refused():
+    r = _run(["--gpus", "2"])
+    assert r.returncode != 0
+    assert r.stdout.strip() == ""
+    assert "visible GPUs" in r.stderr
+
+
+def test_gpus_disagreeing_with_world_size_is_refused():
+    r = _run(["--gpus", "2"], {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0 and r.stdout.strip() == ""
+    assert "WORLD_SIZE" in r.stderr
+
+
+def test_exact_absdiff_count():
+    """roofline.valu bills w*h per block: the 1080p bottom row is 16x8."""
+    sys.path.insert(0, REPO)
+    import bench
+    import motionestimation_amd as me
+    assert bench.exact_absdiffs(1920, 1080, 16, 32) == 8_463_799_296
+    # brute force on a small ragged frame against the per-block definition
+    w, h, blk, span = 70, 45, 16, 9
+    tot = 0
+    for by in range((h + blk - 1) // blk):
+        for bx in range((w + blk - 1) // blk):
+            bw, bh = min(blk, w - bx * blk), min(blk, h - by * blk)
+            tot += bench._block_candidates(w, h, blk, span, bx, by) * bw * bh
+    assert bench.exact_absdiffs(w, h, blk, span) == tot
+    assert me.candidate_count(w, h, blk, span) == sum(
+        bench._block_candidates(w, h, blk, span, bx, by)
+        for by in range(3) for bx in range(5))
+    assert np.isclose(bench.exact_absdiffs(w, h, blk, span, 1, 2),
+                      sum(bench._block_candidates(w, h, blk, span, bx, 1) * min(blk, w - bx * blk) * 16
+                          for bx in range(5)))

@@ -115,6 +115,22 @@ def _bench_ranks(nproc, backend, extra=()):
     return json.loads(lines[0])
 
 
+def _bench_no_launcher(nproc, backend, extra=()):
+    """bench.py --gpus N with no torch.distributed.run around it (the driver's
+    own command line): bench.py starts the N ranks itself."""
+    cmd = [sys.executable, os.path.join(O.REPO, "bench.py"), "--gpus", str(nproc),
+           "--dist-backend", backend, "--steps", "4", "--warmup", "1", "--no-cpu", "--no-ssd",
+           "--no-stream", *extra]
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env["OMP_NUM_THREADS"] = "1"
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = r.stdout.splitlines()
+    assert len(lines) == 1 and lines[0].startswith("{"), r.stdout
+    return json.loads(lines[0])
+
+
 def _check_stripe_line(d, nproc):
     assert d["n_gpus"] == nproc and d["scaling"] == "strong"
     assert d["config"]["parallelism"] == f"stripe{nproc}"
@@ -129,6 +145,13 @@ def test_bench_stripe_mode_two_ranks_gloo_rehearsal():
     one GPU over gloo: each rank's stripe goes through libme_hip.so and the
     gathered 1080p and 4K fields equal a full-frame search."""
     _check_stripe_line(_bench_ranks(2, "gloo"), 2)
+
+
+def test_bench_spawns_its_own_ranks_gloo():
+    """`python bench.py --gpus 2` with no launcher (how the driver runs it):
+    two ranks, started by bench.py itself, in stripe mode with gather parity
+    for the 1080p line and the nested 4K record (gloo: both ranks on one GPU)."""
+    _check_stripe_line(_bench_no_launcher(2, "gloo"), 2)
 
 
 def test_bench_stripe_mode_rccl_one_rank():

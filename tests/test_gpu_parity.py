@@ -182,6 +182,18 @@ def test_c_adapter_fills_reference_block_records(engine, manifest):
     got = np.array([[b.motion_vectorX, b.motion_vectorY] for b in blks])
     np.testing.assert_array_equal(got, gmv)
     assert all(b.is_best_match_found == 1 for b in blks)
+    # planes that did not come from 8-bit samples are refused, not truncated
+    for bad in (256, -1, 1 << 20):
+        r_bad = r32.copy()
+        r_bad[100, 200] = bad
+        st = me._lib.lib().me_find_best_blocks(engine._h, r_bad.ctypes.data, c32.ctypes.data,
+                                               352, 288, 16, 16, blks, n)
+        assert st == me._lib.ME_EINVAL, bad
+        assert b"outside [0, 255]" in me._lib.lib().me_last_error(engine._h)
+        c_bad = c32.copy()
+        c_bad[0, 0] = bad
+        assert me._lib.lib().me_find_best_blocks(engine._h, r32.ctypes.data, c_bad.ctypes.data,
+                                                 352, 288, 16, 16, blks, n) == me._lib.ME_EINVAL
 
 
 def test_error_paths(engine):
