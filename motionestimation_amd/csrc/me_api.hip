@@ -44,14 +44,14 @@ static Tuning read_tuning() {
   if (const char* e = getenv("ME_PLAN")) {
     int v[5] = {0, 0, 0, 0, -1};
     const int n = sscanf(e, "%d,%d,%d,%d,%d", &v[0], &v[1], &v[2], &v[3], &v[4]);
-    const bool ok = n >= 4 && (v[0] == 0 || v[0] == 5 || v[0] == 8 || v[0] == 11 || v[0] == 13) &&
+    const bool ok = n >= 4 && (v[0] == 0 || v[0] == 4 || v[0] == 5 || v[0] == 8 || v[0] == 11 || v[0] == 13) &&
                     v[1] >= 0 && v[1] <= 16 && v[2] >= 0 && v[2] <= 64 &&
                     (v[3] == 0 || (v[3] >= 64 && v[3] <= 1024 && v[3] % 64 == 0)) &&
                     v[4] >= -1 && v[4] <= 1;
     if (ok) {
       t.plan_k = v[0]; t.plan_tb = v[1]; t.plan_cpp = v[2]; t.plan_threads = v[3]; t.plan_fold = v[4];
     } else {
-      fprintf(stderr, "me_hip: ignoring ME_PLAN=%s (K in {0,5,8,11,13}, tb 0..16, cpp 0..64, "
+      fprintf(stderr, "me_hip: ignoring ME_PLAN=%s (K in {0,4,5,8,11,13}, tb 0..16, cpp 0..64, "
                       "threads 0 or 64..1024 step 64, fold -1..1)\n", e);
     }
   }
@@ -63,6 +63,7 @@ static Tuning read_tuning() {
   env_int("ME_STREAM_AHEAD", 1, 9, &t.stream_ahead);
   env_int("ME_FLOW", 0, 1, &t.flow);
   env_int("ME_FLOW_SLOTS", 2, 16, &t.flow_slots);
+  env_int("ME_PRIO", 0, 1, &t.prio);
   return t;
 }
 const Tuning& tuning() {
@@ -169,8 +170,8 @@ SearchArgs make_args(const uint8_t* ref, int ref_row0, const uint8_t* cur, int c
 
 me_status attach_scratch(me_ctx* c, Dev& d, SearchArgs& p, bool cap) {
   p.sched = d.sched;
-  if (p.cost_kind == COST_SSD) {
-    const size_t tiles = mfma_merge_tiles(p);
+  {
+    const size_t tiles = merge_tiles_needed(p);
     if (tiles > d.merge_cap) {
       if (cap) return fail(c, ME_EINVAL, "captured search needs new scratch: run it once uncaptured first");
       (void)hipFree(d.mkeys);

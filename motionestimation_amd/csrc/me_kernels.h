@@ -64,6 +64,7 @@ struct QsadGeom {
                    // column is spread over lanes gi < K, one v_sad_u8 candidate each
   int dyn_tiles;   // dynamic tile pulls when tiles >= dyn_tiles * workgroups (0: never)
   int flow_slots;  // me_flow_kernel: LDS ring slots (0: the persistent item kernel)
+  int prio;        // waves issuing staging raise their issue priority (s_setprio) meanwhile
 };
 
 // Matrix-core SSD path (me_mfma.hip): B = 16, full-height rows [row0, row0 +
@@ -94,6 +95,9 @@ size_t mfma_merge_tiles(const SearchArgs& p);  // tiles the merge buffers must c
 bool plan_mfma_ssd(const SearchArgs& p, MfmaGeom* g);
 hipError_t launch_mfma_ssd(const SearchArgs& p, const MfmaGeom& g, hipStream_t stream);
 size_t mfma_ssd_scratch(const SearchArgs& p);  // 0: path not applicable
+// Tiles of cross-workgroup merge buffers (mkeys: 16 u64 keys each, ~0; mcnt:
+// one u32 counter each, 0) the search of p needs (the MFMA SSD kernels).
+size_t merge_tiles_needed(const SearchArgs& p);
 bool mfma_disabled();
 
 hipError_t launch_search(const SearchArgs& p, hipStream_t stream, int* used_fast);

@@ -274,7 +274,12 @@ __device__ __forceinline__ void qsad_lane(const uint8_t* __restrict__ tile, int 
 // [start, staged, computed, end, hw_id, xcc_id] for tools/stamps.py.
 __device__ unsigned long long g_stamps[8 << 16];
 #define ME_STAMP(slot, v) do { if (threadIdx.x == 0 && wid < (1 << 16)) g_stamps[8 * wid + (slot)] = (v); } while (0)
+// ... and per wave of me_fast_kernel: [start, first item staged, last task
+// loop done, end, hw_id, xcc_id, realtime start, realtime end] (tools/wave_stamps.py)
+__device__ unsigned long long g_wstamps[8 << 14];
+#define ME_WSTAMP(slot, v) do { if ((threadIdx.x & 63) == 0 && wwid < (1 << 14)) g_wstamps[8 * wwid + (slot)] = (v); } while (0)
 #else
+#define ME_WSTAMP(slot, v) do { } while (0)
 #define ME_STAMP(slot, v) do { } while (0)
 #endif
 
@@ -579,9 +584,18 @@ __global__ __launch_bounds__(1024) void me_fast_kernel(SearchArgs p, QsadGeom g)
   int* tq = reinterpret_cast<int*>(smem + 2 * buf_bytes + 128);  // 4-slot ring of tile ids
 #ifdef ME_STAMPS
   const int wid = bid;
+  const int wwid = bid * (int)(blockDim.x >> 6) + (int)(threadIdx.x >> 6);
 #endif
   ME_STAMP(0, __builtin_amdgcn_s_memtime());
   ME_STAMP(6, __builtin_amdgcn_s_memrealtime());
+  ME_WSTAMP(0, __builtin_amdgcn_s_memtime());
+  ME_WSTAMP(6, __builtin_amdgcn_s_memrealtime());
+  // Staging at raised issue priority: the SIMD arbiter otherwise favours the
+  // oldest waves, so the co-resident workgroups already computing starve a
+  // later one's staging address math and it gets its first item late (the
+  // small-stripe "staircase" of DESIGN.md (e): per-wave stamps
+  // profiles/r03c_wave_stamps.txt).
+  if (g.prio) __builtin_amdgcn_s_setprio(3);
   // Dynamic: each workgroup's first two tiles are its static ones (no atomic
   // storm at launch); the counter of band y hands out the band's tiles past
   // its first 2 * n_y.  Own band first; once it is exhausted, steal from the
@@ -628,6 +642,7 @@ __global__ __launch_bounds__(1024) void me_fast_kernel(SearchArgs p, QsadGeom g)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();  // item k staged by every wave; item k-1 fully consumed
     if (k == 0) ME_STAMP(2, __builtin_amdgcn_s_memtime());  // first item staged
+    if (k == 0) ME_WSTAMP(1, __builtin_amdgcn_s_memtime());
     if (dyn && pass == 0 && tid == 0) {  // starting tile ti: pull tile ti + 2
       const int prev = tq[(ti + 1) & 3];
       tq[(ti + 2) & 3] = prev >= 0 ? pull() : -1;
@@ -635,9 +650,11 @@ __global__ __launch_bounds__(1024) void me_fast_kernel(SearchArgs p, QsadGeom g)
     {
       const int ntile = pass + 1 < passes ? tile : tile_at(ti + 1);
       const int npass = pass + 1 < passes ? pass + 1 : 0;
+      if (g.prio) __builtin_amdgcn_s_setprio(3);
       if (ntile >= 0)
         stage_item<B>(p, g, item_of<B, K>(p, g, ntile, npass), smem + ((k + 1) & 1) * buf_bytes,
                       rref, rcur);
+      if (g.prio) __builtin_amdgcn_s_setprio(0);
     }
 #ifdef ME_STAMPS
     nitems++;
@@ -744,6 +761,7 @@ __global__ __launch_bounds__(1024) void me_fast_kernel(SearchArgs p, QsadGeom g)
                   (unsigned long long)make_key(best >> 16, dx, dy));
       }
     }
+    ME_WSTAMP(2, __builtin_amdgcn_s_memtime());  // this wave's tasks of item k done
     if (pass == passes - 1) {
       __syncthreads();  // every task of the tile has folded its key
       if (tid < it.nb) {
@@ -772,6 +790,17 @@ __global__ __launch_bounds__(1024) void me_fast_kernel(SearchArgs p, QsadGeom g)
     }
   }
   ME_STAMP(1, (unsigned long long)nitems);
+#ifdef ME_STAMPS
+  if ((threadIdx.x & 63) == 0 && wwid < (1 << 14)) {
+    unsigned hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    g_wstamps[8 * wwid + 3] = __builtin_amdgcn_s_memtime();
+    g_wstamps[8 * wwid + 4] = hw;
+    g_wstamps[8 * wwid + 5] = xcc;
+    g_wstamps[8 * wwid + 7] = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
   if (dyn && tid == 0) {
     // The last workgroup out re-zeroes the counters for the next launch on
     // this stream (every other workgroup's final pull precedes its arrival).
@@ -904,8 +933,10 @@ __global__ __launch_bounds__(1024) void me_flow_kernel(SearchArgs p, QsadGeom g)
     // 78.4 -> 78.0 us; with the compile-time pitch 79.0 -> 77.3,
     // profiles/r02ae_ab_flow_start.txt).
     for (int i = 0; i < wave; i++) __builtin_amdgcn_s_sleep(10);
+    if (g.prio) __builtin_amdgcn_s_setprio(3);  // see me_fast_kernel
     stage_item_wave<B>(p, g, item_of<B, K>(p, g, tile_of(wave), 0), smem + wave * slot_bytes, rref,
                        rcur);
+    if (g.prio) __builtin_amdgcn_s_setprio(0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0)
       __hip_atomic_store(&ctl->ready[wave], (uint32_t)wave + 1u, __ATOMIC_RELEASE,
@@ -1058,7 +1089,9 @@ __global__ __launch_bounds__(1024) void me_flow_kernel(SearchArgs p, QsadGeom g)
       if (lane == 0) __hip_atomic_store(&ctl->done[slot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       const int kn = kc + NB;
       if (kn < nitems) {
+        if (g.prio) __builtin_amdgcn_s_setprio(3);
         stage_item_wave<B>(p, g, item_of<B, K>(p, g, tile_of(kn), 0), buf, rref, rcur);
+        if (g.prio) __builtin_amdgcn_s_setprio(0);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane == 0)
           __hip_atomic_store(&ctl->ready[slot], (uint32_t)kn + 1u, __ATOMIC_RELEASE,
@@ -1293,6 +1326,8 @@ bool plan_fast(const SearchArgs& p, QsadGeom* g, int* k_out) {
     for (uint32_t x = 0; x < (uint32_t)(g->tb * g->cpp); x++)
       if (nb > 1 && (uint32_t)(((uint64_t)x * m) >> 32) != x / nb) return false;
   }
+  g->prio = tu.prio != 0;
+  g->flow_slots = 0;
   *k_out = bK;
   return true;
 }
@@ -1302,7 +1337,6 @@ bool plan_fast(const SearchArgs& p, QsadGeom* g, int* k_out) {
 // wave-task full), a ring of >= 4 slots in LDS, the ref tile in 16-byte
 // granules, and >= 2 tiles per CU (fewer leave most of the 16 waves idle: the
 // persistent item kernel takes small stripes).
-static constexpr int FLOW_K = 13;
 static constexpr int FLOW_LDS = 160 * 1024 - 1024;
 
 static int cu_count();
@@ -1313,40 +1347,56 @@ bool plan_flow(const SearchArgs& p, QsadGeom* g) {
   // fold (S % 8) and 16-byte tile granules (S % 16).  S <= 32: at 4K +-64 the
   // item kernel's items are already whole waves (8 blocks x 4 chunks x 32
   // groups) and it measured faster (1.086 vs 1.12 ms, profiles/r02p_flow_sweep.txt).
-  // The fold spreads the dx = +S column over lanes gi < K: G = S/2 >= K = 13.
-  if (S < 16 || S % 16 || S > 32 || S / 2 < FLOW_K) return false;
+  // The fold spreads the dx = +S column over lanes gi < K: G = S/2 >= K.
+  if (S < 16 || S % 16 || S > 32) return false;
   if (tuning().flow == 0) return false;
   const int nbx_full = p.width / B;
   if (nbx_full < 1 || p.width % 16 || p.stride % 16 || (uintptr_t)p.ref % 16 || (uintptr_t)p.cur % 16)
     return false;
-  const int D = 2 * S + 1, K = FLOW_K, G = S / 2, chunks = (D + K - 1) / K;
+  const int D = 2 * S + 1, G = S / 2;
   const int rows = p.block_row_end - p.block_row_begin;
-  // The widest tile that still gives >= 6 tiles per CU (fine enough for the
-  // CUs to finish together), else the narrowest that qualifies.
-  int best_tb = 0, best_ns = 0, fine_tb = 0, fine_ns = 0;
-  for (int tb = 1; tb <= 8; tb++) {
-    if ((tb * G * chunks) % 64) continue;
-    if (tuning().plan_tb && tb != tuning().plan_tb) continue;  // tuning build
+  const int cus = cu_count();
+  auto pitch_of = [&](int tb) {
     int pt = ((tb - 1) * B + 4 * G + B + 4 + 15) & ~15;
     if (((pt >> 4) & 1) == 0) pt += 16;
-    const int slot = (chunks * K + B - 1) * pt + tb * B * B;
-    const int ns = min(16, (FLOW_LDS - 16 * tb * 8 - (int)sizeof(int) * 40) / slot);
-    const long tiles = (long)((nbx_full + tb - 1) / tb) * rows;
-    if (ns < 4 || tiles < 2L * cu_count()) continue;
-    if (!best_tb) {
-      best_tb = tb;
-      best_ns = ns;
+    return pt;
+  };
+  auto slots_of = [&](int tb, int K) {
+    const int chunks = (D + K - 1) / K;
+    const int slot = (chunks * K + B - 1) * pitch_of(tb) + tb * B * B;
+    return min(16, (FLOW_LDS - 16 * tb * 8 - (int)sizeof(int) * 40) / slot);
+  };
+  // K = 13, whole tiles per CU, XCD-banded: the widest tile that still gives
+  // >= 6 tiles per CU (fine enough for the CUs to finish together), else the
+  // narrowest with >= 2 per CU (fewer leave most of the 16 waves idle: the
+  // persistent item kernel takes small stripes).
+  const int K = 13;
+  int best_tb = 0, best_ns = 0;
+  if (G >= 13) {
+    const int chunks = (D + 12) / 13;
+    int fine_tb = 0, fine_ns = 0;
+    for (int tb = 1; tb <= 8; tb++) {
+      if ((tb * G * chunks) % 64) continue;
+      if (tuning().plan_tb && tb != tuning().plan_tb) continue;  // tuning build
+      const int ns = slots_of(tb, 13);
+      const long tiles = (long)((nbx_full + tb - 1) / tb) * rows;
+      if (ns < 4 || tiles < 2L * cus) continue;
+      if (!best_tb) {
+        best_tb = tb;
+        best_ns = ns;
+      }
+      if (tiles >= 6L * cus) {
+        fine_tb = tb;
+        fine_ns = ns;
+      }
     }
-    if (tiles >= 6L * cu_count()) {
-      fine_tb = tb;
-      fine_ns = ns;
+    if (fine_tb) {
+      best_tb = fine_tb;
+      best_ns = fine_ns;
     }
-  }
-  if (fine_tb) {
-    best_tb = fine_tb;
-    best_ns = fine_ns;
   }
   if (!best_tb) return false;
+  const int chunks = (D + K - 1) / K;
   QsadGeom& q = *g;
   q.tb = best_tb;
   q.groups = G;
@@ -1354,9 +1404,7 @@ bool plan_flow(const SearchArgs& p, QsadGeom* g) {
   q.cpp = chunks;
   q.fold = 1;
   q.nbx_full = nbx_full;
-  int pt = ((q.tb - 1) * B + 4 * G + B + 4 + 15) & ~15;
-  if (((pt >> 4) & 1) == 0) pt += 16;
-  q.pitch = pt;
+  q.pitch = pitch_of(q.tb);
   q.rows_alloc = chunks * K + B - 1;
   q.tile_bytes = q.rows_alloc * q.pitch;
   q.wg_per_row = (nbx_full + q.tb - 1) / q.tb;
@@ -1378,6 +1426,7 @@ bool plan_flow(const SearchArgs& p, QsadGeom* g) {
   const int slot = q.tile_bytes + q.tb * B * B;
   if (tuning().flow_slots && tuning().flow_slots < best_ns) best_ns = tuning().flow_slots;
   q.flow_slots = best_ns;
+  q.prio = tuning().prio != 0;
   q.lds = best_ns * slot + best_ns * q.tb * 8 + (int)sizeof(int) * 40;
   return q.lds <= 160 * 1024;
 }
@@ -1544,8 +1593,8 @@ static bool cached_flow_plan(const SearchArgs& p, QsadGeom* g) {
     }
   PlanEntry e;
   e.key = key;
-  e.K = FLOW_K;
   e.ok = plan_flow(p, &e.g);
+  e.K = 13;
   cache[next] = e;
   next = (next + 1) % N;
   if (used < N) used++;
@@ -1559,18 +1608,25 @@ static hipError_t launch_flow(const SearchArgs& p, QsadGeom g, int row0, int nro
   g.row0 = row0;
   g.nrows = nrows;
   const int ntiles = g.wg_per_row * nrows;
+  const int nwg = ntiles > cu_count() ? cu_count() : ntiles;  // one per CU, at most one per tile
   // 144: the pitch of the 4-block tiles 1080p +-32 gets (row addresses in
   // the ds_read2 offsets); any other pitch takes the runtime-pitch body
-  const void* fn = g.pitch == 144 ? (const void*)me_flow_kernel<16, FLOW_K, 144>
-                                  : (const void*)me_flow_kernel<16, FLOW_K, 0>;
-  hipError_t e = lds_attr(fn, g.lds);
-  if (e != hipSuccess) return e;
-  const int nwg = ntiles < cu_count() ? ntiles : cu_count();
-  if (g.pitch == 144)
-    hipLaunchKernelGGL((me_flow_kernel<16, FLOW_K, 144>), dim3((unsigned)nwg), dim3(1024), g.lds, stream, p, g);
-  else
-    hipLaunchKernelGGL((me_flow_kernel<16, FLOW_K, 0>), dim3((unsigned)nwg), dim3(1024), g.lds, stream, p, g);
-  return hipGetLastError();
+#define ME_FLOW_CASE(PP)                                                                        \
+  if (PP == 0 || g.pitch == PP) {                                                               \
+    const hipError_t e = lds_attr((const void*)me_flow_kernel<16, 13, PP>, g.lds);              \
+    if (e != hipSuccess) return e;                                                              \
+    hipLaunchKernelGGL((me_flow_kernel<16, 13, PP>), dim3((unsigned)nwg), dim3(1024), g.lds,    \
+                       stream, p, g);                                                           \
+    return hipGetLastError();                                                                   \
+  }
+  ME_FLOW_CASE(144) ME_FLOW_CASE(0)
+#undef ME_FLOW_CASE
+  return hipErrorInvalidValue;
+}
+
+size_t merge_tiles_needed(const SearchArgs& p) {
+  if (p.block_row_end <= p.block_row_begin) return 0;
+  return p.cost_kind == COST_SSD ? mfma_merge_tiles(p) : 0;
 }
 
 static hipError_t launch_valu(const SearchArgs& p, hipStream_t stream, int* used_fast) {
@@ -1649,6 +1705,11 @@ hipError_t launch_search(const SearchArgs& p, hipStream_t stream, int* used_fast
 
 #ifdef ME_STAMPS
 // Diagnostic build only: copy the per-workgroup stamps to the host.
+extern "C" int me_debug_wave_stamps(unsigned long long* out, int n_words) {
+  if (n_words > (8 << 14)) n_words = 8 << 14;
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(me::g_wstamps), (size_t)n_words * 8, 0,
+                                  hipMemcpyDeviceToHost);
+}
 extern "C" int me_debug_stamps(unsigned long long* out, int n_words) {
   if (n_words > (8 << 16)) n_words = 8 << 16;
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(me::g_stamps), (size_t)n_words * 8, 0,

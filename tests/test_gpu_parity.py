@@ -331,3 +331,45 @@ def test_flow_kernel_full_frames(engine):
     omv, ocost, _ = O.full_search(ref, cur, 16, 32, "sad", threads=NT)
     np.testing.assert_array_equal(mvt.cpu().numpy(), omv)
     np.testing.assert_array_equal(cot.cpu().numpy().view(np.uint32), ocost)
+
+
+@pytest.mark.parametrize("span", [16, 32])
+def test_stripes_of_multi_gpu_splits(engine, span):
+    """Every stripe of 3-, 4- and 8-way 1080p splits (the per-rank unit of the
+    multi-GPU search: the persistent item kernel on small stripes, the flow
+    kernel on large ones), a width with a partial last flow tile (121
+    blocks), an all-ties frame, and frames too small to give every CU work;
+    each stripe searched twice (the kernels' counters reset themselves)."""
+    import torch
+    from motionestimation_amd import shard
+    rng = np.random.default_rng(span)
+    frames = [(1920, 1080, "smooth"), (1936, 1080, "noise"), (1920, 1088, "flat"),
+              (352, 288, "smooth"), (96, 64, "noise"), (48, 48, "smooth")]
+    for w, h, kind in frames:
+        if kind == "flat":
+            ref = cur = np.full((h, w), 13, np.uint8)
+        elif kind == "noise":
+            ref = rng.integers(0, 256, (h, w), dtype=np.uint8)
+            cur = rng.integers(0, 256, (h, w), dtype=np.uint8)
+        else:
+            ref, cur = synth.frame_pair(w, h, 21, 3, -5)
+        omv, ocost, _ = O.full_search(ref, cur, 16, span, "sad", threads=NT)
+        worlds = (1, 3, 4, 8) if h >= 1080 else (1, 2)
+        for world in worlds:
+            for st in shard.plan(w, h, 16, span, world):
+                if not st.nblocks:
+                    continue
+                rt = torch.from_numpy(ref[st.ref_y0:st.ref_y1].copy()).cuda()
+                ct = torch.from_numpy(cur[st.cur_y0:st.cur_y1].copy()).cuda()
+                mvt = torch.full((st.nblocks, 2), -9, dtype=torch.int16, device="cuda")
+                cot = torch.zeros(st.nblocks, dtype=torch.int32, device="cuda")
+                for _ in range(2):  # twice: the merge buffers reset themselves
+                    engine.search_stripe_device(rt, st.ref_y0, ct, st.cur_y0, w, h, 16, span,
+                                                "sad", st.row_begin, st.row_end, mvt, cot)
+                torch.cuda.synchronize()
+                b0, b1 = st.row_begin * st.nbx, st.row_end * st.nbx
+                msg = f"{w}x{h} {kind} S{span} {world}-way rows {st.row_begin}:{st.row_end}"
+                np.testing.assert_array_equal(mvt.cpu().numpy(), omv[b0:b1], err_msg=msg)
+                np.testing.assert_array_equal(cot.cpu().numpy().view(np.uint32), ocost[b0:b1],
+                                              err_msg=msg)
+    engine.device_check()

@@ -3,7 +3,7 @@
 (libme_hip_stamps.so): start-up delay to the first task, time spent waiting for
 items, tasks per wave, and how the waves / CUs finish.  Diagnostic only (the
 stamps cost cycles themselves); times in shader cycles unless marked.
-usage: python3 tools/flow_stamps.py"""
+usage: python3 tools/flow_stamps.py [r0:r1 (one stripe's block rows: the split mode)]"""
 import os, sys
 import numpy as np
 import torch
@@ -20,14 +20,21 @@ rt, ct = torch.from_numpy(ref).cuda(), torch.from_numpy(cur).cuda()
 n = me.num_blocks(1920, 1080, 16)
 mv = torch.empty((n, 2), dtype=torch.int16, device="cuda")
 co = torch.empty(n, dtype=torch.int32, device="cuda")
+rows = sys.argv[1] if len(sys.argv) > 1 else ""
 for _ in range(20):
-    eng.full_search_device(rt, ct, 16, 32, "sad", mv, co)
+    if rows:
+        a, b = (int(x) for x in rows.split(":"))
+        eng.search_stripe_device(rt, 0, ct, 0, 1920, 1080, 16, 32, "sad", a, b, mv, co)
+    else:
+        eng.full_search_device(rt, ct, 16, 32, "sad", mv, co)
 torch.cuda.synchronize()
 L = _lib.lib()
 L.me_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
 buf = np.zeros(8 << 16, np.uint64)
 L.me_debug_stamps(buf.ctypes.data, buf.size)
 st = buf.reshape(-1, 8)[:4096].astype(np.int64)
+if os.environ.get("FLOW_STAMPS_SAVE"):  # raw per-wave records for offline analysis
+    np.save(os.environ["FLOW_STAMPS_SAVE"], st)
 st = st[st[:, 0] > 0]
 start, first, end, spin, ntask = st[:, 0], st[:, 1], st[:, 2], st[:, 3], st[:, 4]
 r0, r1 = st[:, 5], st[:, 6]
