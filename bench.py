@@ -2,21 +2,22 @@
 """bench.py -- full-search block matching throughput on MI355X.
 
 Metric (BASELINE.json): 16x16 SAD candidates/sec at 1080p +-32; achieved HBM
-GB/s vs roofline.  One step = one full search of a 1920x1080 Y-frame pair
-(B=16, S=32, SAD, 33,188,832 exact candidates) per rank, inputs resident in
-HBM before the timed region.
+GB/s vs roofline.  One step = full searches of a batch of 1920x1080 Y-frame
+pairs (B=16, S=32, SAD, 33,188,832 exact candidates per frame), inputs
+resident in HBM before the timed region.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--mode auto|frames|stripe]
                   [--config 1080p|4k|8k] [--cost sad|ssd] [--no-cpu]
 
---mode stripe (the default for N > 1, north_star's split): ONE frame per step
-  split into candidate-balanced block-row stripes, one per rank, each rank
-  holding only its stripe + S-row ref halo; the per-stripe MV records are
-  gathered to rank 0 with one RCCL gather per frame inside the timed region
-  (strong scaling).  Frames stream: the gather of frame k runs on
-  RCCL's stream while frame k+1 is searched (double-buffered records).
---mode frames (the default for N = 1, where it is the same single search):
-  each rank searches its own frame pair per step: weak scaling, no collective.
+A step is a batch of --frames-per-step F frames (default 8), searched in one
+launch per rank (me_full_search_batch_device).
+--mode stripe (the default for N > 1, north_star's split): the step's F frames
+  are each split into cost-balanced block-row stripes, one per rank, each rank
+  holding only its stripes + S-row ref halos; the per-stripe MV records of all
+  F frames are gathered to rank 0 with one RCCL gather per step inside the
+  timed region (strong scaling).  Double-buffered records.
+--mode frames (the default for N = 1, where it is the same search): each rank
+  searches its own F frame pairs per step: weak scaling, no collective.
 Every line also carries `stripe_4k`: BASELINE configs[3] (4K +-64) in stripe
 mode on the same ranks, with its gather parity.
 For N > 1: one process per GPU over RCCL.  Under torch.distributed.run
@@ -71,9 +72,14 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16,
                     help="threads of the main CPU-baseline leg (the GPU box's CPU share)")
     ap.add_argument("--no-4k", action="store_true", help="skip the nested stripe_4k record")
-    ap.add_argument("--no-graph", action="store_true",
-                    help="stripe mode over RCCL: enqueue search + gather per frame instead of "
-                         "replaying one captured hipGraph")
+    ap.add_argument("--graph", action="store_true",
+                    help="stripe mode over RCCL: replay search + gather as one captured hipGraph "
+                         "per step instead of two enqueues (measured slower on one GPU)")
+    ap.add_argument("--ramp-ms", type=float, default=100.0,
+                    help="untimed steps for this long before the W warmup steps (GPU clock ramp)")
+    ap.add_argument("--frames-per-step", type=int, default=8,
+                    help="frames searched per step: one batched launch per rank "
+                         "(me_full_search_batch_device) and, in stripe mode, one gather per step")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="nccl = RCCL (production); gloo only to rehearse N ranks on one GPU")
     return ap.parse_args()
@@ -207,6 +213,26 @@ def host_stream(eng, w, h, blk, span, cost, seed, sx, sy, kern_ms, cands_frame):
     return out
 
 
+def single_frame(eng, ref_t, cur_t, blk, span, cost, nb, cands_frame, dev, steps):
+    """One frame per launch on the same resident pair (HIP events on the
+    launch stream): what batching saves is launch gaps and per-launch tails."""
+    import torch
+    mv = torch.empty((nb, 2), dtype=torch.int16, device=dev)
+    co = torch.empty(nb, dtype=torch.int32, device=dev)
+    for _ in range(3):
+        eng.full_search_device(ref_t, cur_t, blk, span, cost, mv, co)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(steps):
+        eng.full_search_device(ref_t, cur_t, blk, span, cost, mv, co)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / steps
+    return {"value": cands_frame / (ms / 1e3), "unit": "candidates/s", "kernel_ms": ms,
+            "steps": steps, "workload": "one frame per launch (me_full_search_device)"}
+
+
 def ssd_beside(eng, ref_t, cur_t, blk, span, nb, cands_frame, dev, steps):
     """The reference's own cost (MSE = SSD / 256) on the same resident frame pair:
     B = 16 SSD runs on the matrix cores (i8 MFMA).  Reported beside `value`."""
@@ -231,27 +257,38 @@ def ssd_beside(eng, ref_t, cur_t, blk, span, nb, cands_frame, dev, steps):
                          "unit": "TFLOP/s", "frac": tops / I8_PEAK_TOPS}}
 
 
+def batch_frames(ref, cur, nframes):
+    """The step's batch: frame 0 is the config's synthetic pair, frame f > 0 the
+    same pair with every row rotated by 37 f columns (distinct block contents,
+    same statistics; no extra seconds of synthesis per frame at 4K)."""
+    return [(ref, cur) if f == 0 else (np.roll(ref, 37 * f, axis=1), np.roll(cur, 37 * f, axis=1))
+            for f in range(nframes)]
+
+
 class StripeRun:
-    """One frame per step in row stripes over the ranks.
+    """F frames per step in row stripes over the ranks.
 
-    Rank r holds its cur stripe and the ref rows with the S-row halo, searches
-    its block rows (me_full_search_stripe_device), and sends its padded
-    records to rank 0 in one gather per frame.  With RCCL the gather is the
-    library's ncclGather, enqueued right after the search on the same stream:
-    the host never waits inside the timed region."""
+    Rank r holds its cur stripe and the ref rows with the S-row halo of each of
+    the step's F frames, searches its block rows of all F in one launch
+    (me_full_search_batch_device), and sends its padded records to rank 0 in
+    one gather per step.  With RCCL the gather is the library's ncclGather,
+    enqueued right after the search on the same stream: the host never waits
+    inside the timed region."""
 
-    def __init__(self, eng, dev, world, rank, gloo, ref, cur, blk, span, cost, graph=True):
+    def __init__(self, eng, dev, world, rank, gloo, frames, blk, span, cost, graph=False):
         import torch
         import torch.distributed as dist
         from motionestimation_amd import shard
-        h, w = ref.shape
+        h, w = frames[0][0].shape
+        F = len(frames)
         self.eng, self.dev, self.world, self.rank, self.gloo = eng, dev, world, rank, gloo
-        self.w, self.h, self.blk, self.span, self.cost = w, h, blk, span, cost
+        self.w, self.h, self.blk, self.span, self.cost, self.nframes = w, h, blk, span, cost, F
         self.stripes = shard.plan(w, h, blk, span, world)
         self.st = st = self.stripes[rank]
-        self.ref_t = torch.from_numpy(ref[st.ref_y0:st.ref_y1].copy()).to(dev)
-        self.cur_t = torch.from_numpy(cur[st.cur_y0:st.cur_y1].copy()).to(dev)
-        self.recs = [torch.zeros((2, st.max_blocks), dtype=torch.int32, device=dev)
+        self.ref_t = torch.from_numpy(np.stack([r[st.ref_y0:st.ref_y1] for r, _ in frames])).to(dev)
+        self.cur_t = torch.from_numpy(np.stack([c[st.cur_y0:st.cur_y1] for _, c in frames])).to(dev)
+        # records: frame f's stripe at [f * nblocks, (f + 1) * nblocks), padded to F * max_blocks
+        self.recs = [torch.zeros((2, F * st.max_blocks), dtype=torch.int32, device=dev)
                      for _ in range(2)]
         cdev = torch.device("cpu") if gloo else dev
         self.i = 0
@@ -265,11 +302,12 @@ class StripeRun:
         # (a one-rank RCCL group under torch.distributed.run takes this path too:
         # the GPU test of the library gather on a one-GPU box)
         self.lib = dist.is_initialized() and not gloo
-        mvs = [r[0].view(torch.int16).view(st.max_blocks, 2) for r in self.recs]
-        self.run_search = [eng.prepared_stripe_search(
+        mvs = [r[0].view(torch.int16).view(F * st.max_blocks, 2) for r in self.recs]
+        self.run_search = [eng.prepared_batch_search(
             self.ref_t, st.ref_y0, self.cur_t, st.cur_y0, w, h, blk, span, cost, st.row_begin,
             st.row_end, mvs[k], self.recs[k][1]) if st.nblocks else (lambda: None)
             for k in range(2)]
+        self.graphs = None
         if self.lib:
             if not eng.comm_ranks:  # one communicator per context (stripe_4k reuses it)
                 uid = torch.zeros(128, dtype=torch.uint8, device=dev)
@@ -281,13 +319,13 @@ class StripeRun:
                          if rank == 0 else None for r in self.recs]
             self.bufs = [list(f) if f is not None else None for f in self.flat]
             self.run_gather = [eng.prepared_gather(self.recs[k], self.flat[k]) for k in range(2)]
-            # One hipGraph per record buffer holding the search and its gather
-            # (me_capture_begin/end): a frame is one graph launch instead of two
-            # enqueues (the search call ~6 us and ncclGather's ~14 us of host
-            # time made the 8-way 1080p step host-bound).  Each is
-            # run once uncaptured first: that sizes the search scratch and sets
-            # up RCCL's connections.
-            self.graphs = None
+            # --graph: one hipGraph per record buffer holding the search and its
+            # gather (me_capture_begin/end), one graph launch per step.  Not the
+            # default: on one GPU a replay cost more than the two direct
+            # enqueues (8-way 1080p stripe step 24.6 vs 22.0 us, search alone
+            # 20.6 vs 15.5 us; hipGraphLaunch's host time, profiles/r03a_step_overhead_graph.jsonl).
+            # Each is run once uncaptured first: that sizes the search scratch
+            # and sets up RCCL's connections.
             if graph and st.nblocks:
                 from motionestimation_amd import MEError
                 stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -330,28 +368,62 @@ class StripeRun:
             return "torch.distributed.gather (gloo rehearsal)"
         return ("me_gather_device (RCCL ncclGather in libme_hip, on the search stream)" +
                 (", search + gather captured in one hipGraph per record buffer"
-                 if getattr(self, "graphs", None) else ""))
+                 if self.graphs else ""))
 
-    def gathered_field(self):
-        """A last, synchronous frame; rank 0 returns the assembled (mv, cost)."""
+    def gathered_fields(self):
+        """A last, synchronous step; rank 0 returns [(mv, cost)] per frame."""
         import torch
         from motionestimation_amd import shard
         k = self.step()
         torch.cuda.synchronize()
         if self.rank != 0:
             return None
-        if self.world == 1 and not self.lib:
-            rec = self.recs[k].cpu()
-            return shard.assemble([rec], self.stripes)
-        return shard.assemble(self.bufs[k], self.stripes)
+        recs = [self.recs[k].cpu()] if self.world == 1 and not self.lib else self.bufs[k]
+        out = []
+        for f in range(self.nframes):
+            per_rank = []
+            for st, rec in zip(self.stripes, recs):
+                rec = np.asarray(rec.cpu() if hasattr(rec, "cpu") else rec)
+                n = st.nblocks
+                per_rank.append(rec[:, f * n:(f + 1) * n])
+            out.append(shard.assemble(per_rank, self.stripes))
+        return out
 
 
-def timed(step, steps, warmup, world, finish=None):
-    """W untimed steps, then K steps between barrier + synchronize; returns
-    (max-over-ranks wall seconds, max-over-ranks ms per step on the current
-    stream from one HIP event pair around the region)."""
+def clock_ramp(step, ms, world):
+    """Untimed steps until `ms` of wall time has passed on every rank (ranks
+    agree through a MIN all-reduce, so a collective inside the step runs the
+    same number of times everywhere).  The GPU's clock ramps up under load:
+    back-to-back 1080p searches run 76 -> 69 us over the first ~25 ms, and again
+    after 1 s idle (tools/dbg/ramp_probe.py, profiles/r03m_clock_ramp.json).
+    Returns the steps run."""
     import torch
     import torch.distributed as dist
+    t0, n = time.perf_counter(), 0
+    while ms > 0:
+        for _ in range(4):
+            step()
+        n += 4
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        if world > 1:
+            gloo = dist.get_backend() == "gloo"
+            t = torch.tensor([el], dtype=torch.float64,
+                             device="cpu" if gloo else torch.device("cuda", torch.cuda.current_device()))
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            el = float(t[0])
+        if el * 1e3 >= ms:
+            break
+    return n
+
+
+def timed(step, steps, warmup, world, finish=None, ramp_ms=0):
+    """The clock ramp (clock_ramp), W untimed steps, then K steps between
+    barrier + synchronize; returns (max-over-ranks wall seconds, max-over-ranks
+    ms per step on the current stream from one HIP event pair around the region)."""
+    import torch
+    import torch.distributed as dist
+    clock_ramp(step, ramp_ms, world)
     for _ in range(warmup):
         step()
     if finish:
@@ -382,42 +454,48 @@ def timed(step, steps, warmup, world, finish=None):
     return elapsed, kern_ms
 
 
-def stripe_parity(eng, sr, ref, cur, dev):
-    """Rank 0: the gathered stripe field equals one full-frame search (not timed)."""
+def stripe_parity(eng, sr, frames, dev):
+    """Rank 0: the gathered stripe fields of every frame of the step equal one
+    batched full-frame search on one GPU (not timed)."""
     import torch
-    field = sr.gathered_field()
+    import motionestimation_amd as me
+    fields = sr.gathered_fields()
     if sr.rank != 0:
         return None
-    gmv, gcost = field
-    h, w = ref.shape
-    import motionestimation_amd as me
+    h, w = frames[0][0].shape
     nb = me.num_blocks(w, h, sr.blk)
-    fmv = torch.empty((nb, 2), dtype=torch.int16, device=dev)
-    fco = torch.empty(nb, dtype=torch.int32, device=dev)
-    eng.full_search_device(torch.from_numpy(ref).to(dev), torch.from_numpy(cur).to(dev), sr.blk,
-                           sr.span, sr.cost, fmv, fco)
+    F = len(frames)
+    fmv = torch.empty((F * nb, 2), dtype=torch.int16, device=dev)
+    fco = torch.empty(F * nb, dtype=torch.int32, device=dev)
+    eng.search_batch_device(torch.from_numpy(np.stack([r for r, _ in frames])).to(dev), 0,
+                            torch.from_numpy(np.stack([c for _, c in frames])).to(dev), 0, w, h,
+                            sr.blk, sr.span, sr.cost, 0, (h + sr.blk - 1) // sr.blk, fmv, fco)
     torch.cuda.synchronize()
-    return bool(np.array_equal(gmv, fmv.cpu().numpy()) and
-                np.array_equal(gcost, fco.cpu().numpy().view(np.uint32)))
+    fmv, fco = fmv.cpu().numpy(), fco.cpu().numpy().view(np.uint32)
+    return all(np.array_equal(gmv, fmv[f * nb:(f + 1) * nb]) and
+               np.array_equal(gcost, fco[f * nb:(f + 1) * nb])
+               for f, (gmv, gcost) in enumerate(fields))
 
 
-def stripe_record(eng, dev, world, rank, gloo, cfg_name, cost, steps, warmup, graph=True):
+def stripe_record(eng, dev, world, rank, gloo, cfg_name, cost, steps, warmup, nframes,
+                  graph=False, ramp_ms=0):
     """Nested record: a BASELINE config in stripe mode on the same ranks."""
     import motionestimation_amd as me
     from motionestimation_amd import synth
     cfg, blk, span = CONFIGS[cfg_name]
     w, h, seed, sx, sy = synth.CONFIGS[cfg]
-    ref, cur = synth.frame_pair(w, h, seed, sx, sy)
+    frames = batch_frames(*synth.frame_pair(w, h, seed, sx, sy), nframes)
     cands = me.candidate_count(w, h, blk, span)
-    sr = StripeRun(eng, dev, world, rank, gloo, ref, cur, blk, span, cost, graph)
-    elapsed, kern_ms = timed(sr.step, steps, warmup, world)
-    parity = stripe_parity(eng, sr, ref, cur, dev)
-    return {"value": cands * steps / elapsed, "unit": "candidates/s",
-            "frames_per_s": steps / elapsed, "ms_per_step": elapsed / steps * 1e3,
+    sr = StripeRun(eng, dev, world, rank, gloo, frames, blk, span, cost, graph)
+    elapsed, kern_ms = timed(sr.step, steps, warmup, world, ramp_ms=ramp_ms)
+    parity = stripe_parity(eng, sr, frames, dev)
+    return {"value": cands * nframes * steps / elapsed, "unit": "candidates/s",
+            "frames_per_s": nframes * steps / elapsed, "ms_per_step": elapsed / steps * 1e3,
             "kernel_ms": kern_ms, "steps": steps, "warmup": warmup, "n_gpus": world,
-            "scaling": "strong", "parallelism": f"stripe{world}",
+            "frames_per_step": nframes, "scaling": "strong", "parallelism": f"stripe{world}",
             "workload": f"{w}x{h} Y, {blk}x{blk} blocks, full search +-{span}, {cost.upper()}, "
-                        "one frame per step in row stripes + one RCCL gather per frame",
+                        f"{nframes} frames per step, each in row stripes over the ranks; one "
+                        "batched search and one RCCL gather per step",
             "candidates_per_frame": cands, "stripe_gather_parity": parity,
             "gather": sr.gather_impl()}
 
@@ -528,30 +606,32 @@ def main():
     eng = me.Engine(devices=[gpu])
 
     mode = args.mode if args.mode != "auto" else ("frames" if world == 1 else "stripe")
+    F = args.frames_per_step
     parity = None
     if mode == "frames":
-        # rank r: its own frame pair of the sequence (same size; seed varies)
+        # rank r: its own batch of F frame pairs (same size; seed varies), all F
+        # searched in one launch per step (me_full_search_batch_device)
         ref, cur = synth.frame_pair(w, h, seed + rank, sx, sy)
-        ref_t = torch.from_numpy(ref).to(dev)
-        cur_t = torch.from_numpy(cur).to(dev)
-        mv_t = torch.empty((nb, 2), dtype=torch.int16, device=dev)
-        cost_t = torch.empty(nb, dtype=torch.int32, device=dev)
-
-        def step():
-            eng.full_search_device(ref_t, cur_t, blk, span, args.cost, mv_t, cost_t)
-        units_per_step = cands_frame * world
+        frames = batch_frames(ref, cur, F)
+        ref_t = torch.from_numpy(np.stack([r for r, _ in frames])).to(dev)
+        cur_t = torch.from_numpy(np.stack([c for _, c in frames])).to(dev)
+        mv_t = torch.empty((F * nb, 2), dtype=torch.int16, device=dev)
+        cost_t = torch.empty(F * nb, dtype=torch.int32, device=dev)
+        step = eng.prepared_batch_search(ref_t, 0, cur_t, 0, w, h, blk, span, args.cost, 0,
+                                         (h + blk - 1) // blk, mv_t, cost_t)
+        units_per_step = cands_frame * F * world
         # Kernel duration: one HIP event pair on the stream the search is
         # launched on (torch's current stream) around the whole timed region,
         # / K (per-step event pairs would stretch the back-to-back launches).
-        elapsed, kern_ms = timed(step, args.steps, args.warmup, world)
+        elapsed, kern_ms = timed(step, args.steps, args.warmup, world, ramp_ms=args.ramp_ms)
     else:
         ref, cur = synth.frame_pair(w, h, seed, sx, sy)
-        sr = StripeRun(eng, dev, world, rank, gloo, ref, cur, blk, span, args.cost,
-                       not args.no_graph)
+        frames = batch_frames(ref, cur, F)
+        sr = StripeRun(eng, dev, world, rank, gloo, frames, blk, span, args.cost, args.graph)
         st = sr.st
-        units_per_step = cands_frame
-        elapsed, kern_ms = timed(sr.step, args.steps, args.warmup, world)
-        parity = stripe_parity(eng, sr, ref, cur, dev)
+        units_per_step = cands_frame * F
+        elapsed, kern_ms = timed(sr.step, args.steps, args.warmup, world, ramp_ms=args.ramp_ms)
+        parity = stripe_parity(eng, sr, frames, dev)
 
     value = units_per_step * args.steps / elapsed
     # Roofline of the dominant kernel: algorithmic HBM bytes per
@@ -559,12 +639,13 @@ def main():
     # for the planes that launch covers.
     # VALU work: the exact abs-diff count (w*h of each block, not B*B).
     # Stripe mode: the frame's work / N against the slowest rank's kernel time.
+    # A launch searches the step's F frames (F stripes in stripe mode).
     if mode == "frames":
-        alg_bytes = 2 * w * h + 8 * nb
-        absdiffs = exact_absdiffs(w, h, blk, span)
+        alg_bytes = F * (2 * w * h + 8 * nb)
+        absdiffs = F * exact_absdiffs(w, h, blk, span)
     else:
-        alg_bytes = (st.ref_y1 - st.ref_y0 + st.cur_y1 - st.cur_y0) * w + 8 * st.nblocks
-        absdiffs = exact_absdiffs(w, h, blk, span) / world
+        alg_bytes = F * ((st.ref_y1 - st.ref_y0 + st.cur_y1 - st.cur_y0) * w + 8 * st.nblocks)
+        absdiffs = F * exact_absdiffs(w, h, blk, span) / world
     achieved = alg_bytes / (kern_ms / 1e3) / 1e9
     tag = f"{args.config}_b{blk}_s{span}_{args.cost}"
     traffic, traffic_search = load_traffic(tag)
@@ -577,6 +658,7 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
+        "clock_ramp_ms": args.ramp_ms,
         "higher_is_better": True,
         "scaling": "weak" if mode == "frames" else "strong",
         "vs_baseline": None,
@@ -585,10 +667,14 @@ def main():
                 f"{'+rank' if mode == 'frames' and world > 1 else ''}, 5x5 box, cur = ref shifted "
                 f"({sx:+d},{sy:+d}) + uniform [-2,2])",
         "config": {"workload": f"{w}x{h} Y, {blk}x{blk} blocks, full search +-{span}, "
-                               f"{args.cost.upper()}, {'one frame pair per rank per step' if mode == 'frames' else 'one frame per step in row stripes + one RCCL gather per frame'}",
+                               f"{args.cost.upper()}, " +
+                               (f"{F} frame pairs per rank per step in one batched search"
+                                if mode == "frames" else
+                                f"{F} frames per step, each in row stripes over the ranks; one "
+                                "batched search and one RCCL gather per step"),
                    "width": w, "height": h, "block": blk, "range": span, "cost": args.cost,
                    "candidates_per_frame": cands_frame, "blocks_per_frame": nb,
-                   "parallelism": f"{mode}{world}"},
+                   "frames_per_step": F, "parallelism": f"{mode}{world}"},
         "kernel_ms": kern_ms,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
@@ -615,9 +701,14 @@ def main():
                                     "(S2 prepass + MFMA kernel); dense i8 peak",
                             "hbm": {k: hbm[k] for k in ("achieved", "peak", "unit", "frac",
                                                         "algorithmic_bytes_per_launch")}}
+    if rank == 0 and world == 1 and mode == "frames" and F > 1:
+        # the same search one frame per launch (me_full_search_device), for
+        # comparison: the batch's only difference is launches per frame
+        line["single_frame"] = single_frame(eng, ref_t[0], cur_t[0], blk, span, args.cost, nb,
+                                            cands_frame, dev, min(args.steps * F, 100))
     if (rank == 0 and world == 1 and mode == "frames" and args.cost == "sad"
             and blk == 16 and not args.no_ssd):
-        line["ssd_mfma"] = ssd_beside(eng, ref_t, cur_t, blk, span, nb, cands_frame, dev,
+        line["ssd_mfma"] = ssd_beside(eng, ref_t[0], cur_t[0], blk, span, nb, cands_frame, dev,
                                       min(args.steps, 20))
     if parity is not None:
         line["stripe_gather_parity"] = parity
@@ -629,7 +720,8 @@ def main():
         # BASELINE configs[3] (4K +-64), the config north_star's 8-GPU split is
         # quoted on, in stripe mode on the same ranks (at N = 1: the denominator)
         rec4k = stripe_record(eng, dev, world, rank, gloo, "4k", args.cost,
-                              min(args.steps, 20), min(args.warmup, 3), not args.no_graph)
+                              min(args.steps, 20), min(args.warmup, 3), F, args.graph,
+                              min(args.ramp_ms, 30.0))
         if rank == 0:
             line["stripe_4k"] = rec4k
     if rank == 0 and world == 1 and mode == "frames" and not args.no_stream:

@@ -143,6 +143,27 @@ me_status me_full_search_stripe_device(me_ctx* ctx, const uint8_t* d_ref,
                                        int16_t* d_mv_xy, uint32_t* d_block_cost,
                                        void* stream);
 
+/* A batch of n_frames stripes (or whole frames: block rows [0, nby)) in one
+ * launch.  Frame f's ref rows start at d_ref + f * ref_frame_stride bytes and
+ * its cur rows at d_cur + f * cur_frame_stride; every frame has the geometry,
+ * row pitch, block rows and resident-row contract of
+ * me_full_search_stripe_device (ref_row0 / cur_row0 are the frame rows of each
+ * frame's first resident row).  Frame f's records are written at
+ * d_mv_xy + 2 * f * nblk and d_block_cost + f * nblk, nblk = (block_row_end -
+ * block_row_begin) * ceil(W/B).  Results are those of one
+ * me_full_search_stripe_device per frame; a batch fills the GPU where one small
+ * stripe cannot (the per-rank step of a multi-GPU split over several frames:
+ * one launch and one gather for all of them).  The whole batch stays below
+ * 2 GiB per plane stack (ME_EUNSUPPORTED otherwise). */
+me_status me_full_search_batch_device(me_ctx* ctx, const uint8_t* d_ref,
+                                      size_t ref_frame_stride, int ref_row0,
+                                      const uint8_t* d_cur, size_t cur_frame_stride,
+                                      int cur_row0, int width, int height, int stride,
+                                      int block_size, int search_range, me_cost cost,
+                                      int block_row_begin, int block_row_end, int n_frames,
+                                      int16_t* d_mv_xy, uint32_t* d_block_cost,
+                                      void* stream);
+
 /* Balanced stripe plan: bounds[0..n_shards] block-row boundaries, each stripe
  * carrying about the same search cost.  The cost of a block row is its block
  * count times (3 * (2S+1) + ny) / 4, ny = its exact candidate-row count: the

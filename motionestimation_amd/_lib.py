@@ -41,6 +41,10 @@ _SIGS = {
     "me_full_search_stripe_device": (ctypes.c_int, [ctypes.c_void_p, _u8p, ctypes.c_int, _u8p,
                                                     ctypes.c_int] + [ctypes.c_int] * 8 +
                                      [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "me_full_search_batch_device": (ctypes.c_int, [ctypes.c_void_p, _u8p, ctypes.c_size_t,
+                                                   ctypes.c_int, _u8p, ctypes.c_size_t] +
+                                    [ctypes.c_int] * 10 +
+                                    [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "me_plan_stripes": (ctypes.c_int, [ctypes.c_int] * 5 + [ctypes.POINTER(ctypes.c_int)]),
     "me_comm_unique_id": (ctypes.c_int, [ctypes.c_void_p]),
     "me_comm_init": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),

@@ -159,6 +159,11 @@ SearchArgs make_args(const uint8_t* ref, int ref_row0, const uint8_t* cur, int c
   const long ref_rows = ref_end - ref_row0, cur_rows = cur_end - cur_row0;
   p.ref_bytes = ref_rows > 0 ? (uint32_t)((ref_rows - 1) * (long)stride + width) : 0;
   p.cur_bytes = cur_rows > 0 ? (uint32_t)((cur_rows - 1) * (long)stride + width) : 0;
+  p.ref_bytes1 = p.ref_bytes;
+  p.cur_bytes1 = p.cur_bytes;
+  p.nframes = 1;
+  p.ref_fstride = p.cur_fstride = 0;
+  p.out_fstride = (r1 - r0) * p.nbx;
   p.sched = nullptr;
   p.scratch = nullptr;
   p.scratch_bytes = 0;
@@ -644,6 +649,43 @@ me_status me_full_search_stripe_device(me_ctx* c, const uint8_t* d_ref, int ref_
   c->err[0] = 0;
   me::SearchArgs p = make_args(d_ref, ref_row0, d_cur, cur_row0, width, height, stride, blk,
                                range, cost, r0, r1, d_mv, d_cost);
+  const bool cap = me::capturing((hipStream_t)stream);
+  if ((s = attach_scratch(c, c->devs[0], p, cap)) != ME_OK) return s;
+  return launch_ordered(c, c->devs[0], p, (hipStream_t)stream);
+}
+
+me_status me_full_search_batch_device(me_ctx* c, const uint8_t* d_ref, size_t ref_frame_stride,
+                                     int ref_row0, const uint8_t* d_cur, size_t cur_frame_stride,
+                                     int cur_row0, int width, int height, int stride, int blk,
+                                     int range, me_cost cost, int r0, int r1, int n_frames,
+                                     int16_t* d_mv, uint32_t* d_cost, void* stream) {
+  me_status s = check_args(c, d_ref, d_cur, width, height, stride, blk, range, cost, d_mv);
+  if (s != ME_OK) return s;
+  const int nby = (height + blk - 1) / blk;
+  if (r0 < 0 || r1 > nby || r0 > r1) return fail(c, ME_EINVAL, "block rows [%d, %d)", r0, r1);
+  if (n_frames < 1) return fail(c, ME_EINVAL, "n_frames %d", n_frames);
+  const int need_ref0 = r0 * blk - range > 0 ? r0 * blk - range : 0;
+  if (ref_row0 < 0 || ref_row0 > need_ref0) return fail(c, ME_EINVAL, "ref_row0 %d", ref_row0);
+  if (cur_row0 < 0 || cur_row0 > r0 * blk) return fail(c, ME_EINVAL, "cur_row0 %d", cur_row0);
+  c->err[0] = 0;
+  me::SearchArgs p = make_args(d_ref, ref_row0, d_cur, cur_row0, width, height, stride, blk,
+                               range, cost, r0, r1, d_mv, d_cost);
+  if (n_frames > 1) {
+    // every frame's resident rows inside its stride; the batch addressable
+    // with 32-bit offsets (buffer descriptors)
+    if (ref_frame_stride < p.ref_bytes1 || cur_frame_stride < p.cur_bytes1)
+      return fail(c, ME_EINVAL, "frame strides %zu / %zu below a frame's %u / %u bytes",
+                  ref_frame_stride, cur_frame_stride, p.ref_bytes1, p.cur_bytes1);
+    const unsigned long long rb = (unsigned long long)(n_frames - 1) * ref_frame_stride + p.ref_bytes1;
+    const unsigned long long cb = (unsigned long long)(n_frames - 1) * cur_frame_stride + p.cur_bytes1;
+    if (rb >= (1ull << 31) || cb >= (1ull << 31))
+      return fail(c, ME_EUNSUPPORTED, "batch of %llu / %llu bytes (limit 2 GiB)", rb, cb);
+    p.nframes = n_frames;
+    p.ref_fstride = (uint32_t)ref_frame_stride;
+    p.cur_fstride = (uint32_t)cur_frame_stride;
+    p.ref_bytes = (uint32_t)rb;
+    p.cur_bytes = (uint32_t)cb;
+  }
   const bool cap = me::capturing((hipStream_t)stream);
   if ((s = attach_scratch(c, c->devs[0], p, cap)) != ME_OK) return s;
   return launch_ordered(c, c->devs[0], p, (hipStream_t)stream);

@@ -31,6 +31,14 @@ struct SearchArgs {
   uint32_t* cost;
   uint32_t ref_bytes;  // readable bytes from ref (buffer range check), and from cur
   uint32_t cur_bytes;
+  // Batch of nframes frames (me_full_search_batch_device): frame f's planes
+  // start f * ref_fstride / cur_fstride bytes after ref / cur, its records
+  // f * out_fstride blocks after mv / cost; ref_bytes / cur_bytes cover the
+  // whole batch, ref_bytes1 / cur_bytes1 one frame.  nframes = 1 otherwise.
+  int nframes;
+  uint32_t ref_fstride, cur_fstride;
+  int out_fstride;
+  uint32_t ref_bytes1, cur_bytes1;
   uint32_t* sched;     // 16 u32: [0, 9) zeroed tile counters + arrivals (8 XCD groups),
                        // [SCHED_ERR] the invariant word; or null
   uint8_t* scratch;    // device scratch of the MFMA SSD path (mfma_ssd_scratch bytes) or null

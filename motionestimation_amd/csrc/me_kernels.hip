@@ -475,15 +475,24 @@ __device__ __forceinline__ void dma4(__amdgpu_buffer_rsrc_t rs, uint8_t* lds_dst
   }
 }
 
-// Geometry of one work item = (tile of TB blocks, dy pass).
+// Geometry of one work item = (tile of TB blocks, dy pass); in a batched
+// launch (p.nframes > 1, the flow kernel) tiles run frame-major and f is the
+// item's frame: its planes start f * p.ref_fstride / cur_fstride bytes on and
+// its records f * p.out_fstride blocks on.
 struct Item {
-  int bx0, by, nb, tly, h, a, X0, c0, nch, prow0, prows;
+  int bx0, by, nb, tly, h, a, X0, c0, nch, prow0, prows, f;
 };
 
 template <int B, int K>
 __device__ __forceinline__ Item item_of(const SearchArgs& p, const QsadGeom& g, int tile,
                                         int pass) {
   Item it;
+  it.f = 0;
+  if (p.nframes > 1) {
+    const int tpf = g.wg_per_row * g.nrows;  // tiles per frame
+    it.f = tile / tpf;
+    tile -= it.f * tpf;
+  }
   it.bx0 = (tile % g.wg_per_row) * g.tb;
   it.by = g.row0 + tile / g.wg_per_row;
   it.nb = min(g.tb, g.nbx_full - it.bx0);
@@ -856,7 +865,7 @@ __device__ __forceinline__ void stage_item_wave(const SearchArgs& p, const QsadG
   uint8_t* tile = buf;
   uint8_t* cur = buf + g.tile_bytes;
   const int pitch = g.pitch, stride = p.stride;
-  const int base = (it.prow0 - p.ref_row0) * stride + it.X0;
+  const uint32_t base = (uint32_t)it.f * p.ref_fstride + (uint32_t)((it.prow0 - p.ref_row0) * stride + it.X0);
   const int bytes = it.prows * pitch;
   for (int s0 = 0; s0 < bytes; s0 += 1024) {  // 16-byte granules (g.tile16)
     const int d = s0 + 16 * lane;
@@ -864,16 +873,16 @@ __device__ __forceinline__ void stage_item_wave(const SearchArgs& p, const QsadG
     if (d < bytes)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
           rref, (__attribute__((address_space(3))) void*)(tile + s0), 16,
-          (uint32_t)(base + r * stride + x), 0, 0, 0);
+          base + (uint32_t)(r * stride + x), 0, 0, 0);
   }
-  const int cbase = (it.tly - p.cur_row0) * stride + it.bx0 * B;
+  const uint32_t cbase = (uint32_t)it.f * p.cur_fstride + (uint32_t)((it.tly - p.cur_row0) * stride + it.bx0 * B);
   const int cb = it.nb * B * B;
   for (int s0 = 0; s0 < cb; s0 += 1024) {
     const int d = s0 + 16 * lane;
     if (d < cb)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
           rcur, (__attribute__((address_space(3))) void*)(cur + s0), 16,
-          (uint32_t)(cbase + ((d >> 4) & 15) * stride + (d >> 8) * B), 0, 0, 0);
+          cbase + (uint32_t)(((d >> 4) & 15) * stride + (d >> 8) * B), 0, 0, 0);
   }
 }
 
@@ -906,8 +915,8 @@ __global__ __launch_bounds__(1024) void me_flow_kernel(SearchArgs p, QsadGeom g)
       __builtin_amdgcn_make_buffer_rsrc((void*)p.cur, (short)0, p.cur_bytes, 0x00020000);
 
   // This workgroup's tiles: the XCD band of bid % 8 (a speed heuristic only),
-  // member m takes tiles band0 + m, + n_x, ...
-  const int ntiles = g.wg_per_row * g.nrows;
+  // member m takes tiles band0 + m, + n_x, ... (all frames of a batch, frame-major)
+  const int ntiles = g.wg_per_row * g.nrows * p.nframes;
   const int nwg = (int)gridDim.x, bid = (int)blockIdx.x;
   const int ng = nwg < 8 ? nwg : 8;
   const int x = bid % ng, m = bid / ng;
@@ -1081,7 +1090,7 @@ __global__ __launch_bounds__(1024) void me_flow_kernel(SearchArgs p, QsadGeom g)
       if (lane < it.nb) {
         const uint64_t kk = keys[slot * g.tb + lane];
         keys[slot * g.tb + lane] = ~0ull;
-        const int out = (it.by - p.block_row_begin) * p.nbx + it.bx0 + lane;
+        const int out = it.f * p.out_fstride + (it.by - p.block_row_begin) * p.nbx + it.bx0 + lane;
         p.mv[2 * out] = (int16_t)((int)(kk & 0xFFFF) - 32768);
         p.mv[2 * out + 1] = (int16_t)((int)((kk >> 16) & 0xFFFF) - 32768);
         if (p.cost) p.cost[out] = (uint32_t)(kk >> 32);
@@ -1351,10 +1360,11 @@ bool plan_flow(const SearchArgs& p, QsadGeom* g) {
   if (S < 16 || S % 16 || S > 32) return false;
   if (tuning().flow == 0) return false;
   const int nbx_full = p.width / B;
-  if (nbx_full < 1 || p.width % 16 || p.stride % 16 || (uintptr_t)p.ref % 16 || (uintptr_t)p.cur % 16)
+  if (nbx_full < 1 || p.width % 16 || p.stride % 16 || (uintptr_t)p.ref % 16 || (uintptr_t)p.cur % 16 ||
+      p.ref_fstride % 16 || p.cur_fstride % 16)
     return false;
   const int D = 2 * S + 1, G = S / 2;
-  const int rows = p.block_row_end - p.block_row_begin;
+  const int rows = (p.block_row_end - p.block_row_begin) * p.nframes;  // every frame of a batch
   const int cus = cu_count();
   auto pitch_of = [&](int tb) {
     int pt = ((tb - 1) * B + 4 * G + B + 4 + 15) & ~15;
@@ -1393,6 +1403,16 @@ bool plan_flow(const SearchArgs& p, QsadGeom* g) {
     if (fine_tb) {
       best_tb = fine_tb;
       best_ns = fine_ns;
+    }
+    // tb = 4 (the 144-byte pitch compiled into the kernel: row addresses in
+    // the ds_read2 offsets) whenever it gives >= 6 tiles per CU: a batch of
+    // 8 1080p frames took tb = 8 at the runtime pitch, 84 us per frame
+    // against 69-78 for single frames (profiles/r03j_*)
+    const long tiles4 = (long)((nbx_full + 3) / 4) * rows;
+    if (best_tb != 4 && (4 * G * chunks) % 64 == 0 && pitch_of(4) == 144 && slots_of(4, 13) >= 4 &&
+        tiles4 >= 6L * cus && !tuning().plan_tb) {
+      best_tb = 4;
+      best_ns = slots_of(4, 13);
     }
   }
   if (!best_tb) return false;
@@ -1536,9 +1556,11 @@ hipError_t launch_fast(const SearchArgs& p, QsadGeom g, int K, int row0, int nro
 // them) so a steady stream of same-shape searches pays the planner once.
 struct PlanKey {
   int width, height, stride, blk, range, cost, rows, aligned;  // aligned: 1 (4 B) | 2 (16 B)
+  int nframes = 1;
   bool operator==(const PlanKey& o) const {
     return width == o.width && height == o.height && stride == o.stride && blk == o.blk &&
-           range == o.range && cost == o.cost && rows == o.rows && aligned == o.aligned;
+           range == o.range && cost == o.cost && rows == o.rows && aligned == o.aligned &&
+           nframes == o.nframes;
   }
 };
 struct PlanEntry {
@@ -1582,9 +1604,11 @@ static bool cached_flow_plan(const SearchArgs& p, QsadGeom* g) {
   static int used = 0, next = 0;
   static std::mutex mu;
   const int aligned = ((p.stride % 16 == 0) && ((uintptr_t)p.ref % 16 == 0) &&
-                       ((uintptr_t)p.cur % 16 == 0)) ? 3 : 0;
-  const PlanKey key{p.width, p.height, p.stride, p.blk, p.range, p.cost_kind,
-                    p.block_row_end - p.block_row_begin, aligned};
+                       ((uintptr_t)p.cur % 16 == 0) && (p.ref_fstride % 16 == 0) &&
+                       (p.cur_fstride % 16 == 0)) ? 3 : 0;
+  PlanKey key{p.width, p.height, p.stride, p.blk, p.range, p.cost_kind,
+              p.block_row_end - p.block_row_begin, aligned};
+  key.nframes = p.nframes;
   std::lock_guard<std::mutex> lk(mu);
   for (int i = 0; i < used; i++)
     if (cache[i].key == key) {
@@ -1671,10 +1695,83 @@ static hipError_t launch_valu(const SearchArgs& p, hipStream_t stream, int* used
   return hipSuccess;
 }
 
+// Frame f of a batch as a single-frame search.
+static SearchArgs frame_args(const SearchArgs& p, int f) {
+  SearchArgs q = p;
+  q.nframes = 1;
+  q.ref = p.ref + (size_t)f * p.ref_fstride;
+  q.cur = p.cur + (size_t)f * p.cur_fstride;
+  q.ref_bytes = p.ref_bytes1;
+  q.cur_bytes = p.cur_bytes1;
+  q.ref_fstride = q.cur_fstride = 0;
+  q.mv = p.mv + 2 * (size_t)f * p.out_fstride;
+  if (p.cost) q.cost = p.cost + (size_t)f * p.out_fstride;
+  return q;
+}
+
 hipError_t launch_search(const SearchArgs& p, hipStream_t stream, int* used_fast) {
   const int r0 = p.block_row_begin, r1 = p.block_row_end;
-  if (r1 <= r0) return hipSuccess;
+  if (r1 <= r0 || p.nframes < 1) return hipSuccess;
   if (used_fast) *used_fast = 0;
+  if (p.nframes > 1) {
+    // A batch: one flow-kernel launch over every frame's full-height rows
+    // (frame-major tiles) where the flow kernel takes the search; the rest
+    // (other costs and shapes, a frame's odd bottom row or partial right
+    // column) frame by frame.
+    QsadGeom g;
+    if (p.cost_kind == COST_SAD && cached_flow_plan(p, &g)) {
+      const int nby = (p.height + p.blk - 1) / p.blk;
+      const int h_last = p.height - (nby - 1) * p.blk;
+      int rq1 = r1;
+      if (r1 == nby && h_last != p.blk && h_last != p.blk / 2) rq1 = r1 - 1;
+      // At most one ring of tiles per CU per launch: every item is then staged
+      // at the start.  Past the ring, refills under compute starved the waves
+      // (a batch of 8 1080p frames: 22 % of wave time spinning on unpublished
+      // slots, 87 us per frame against 69 for single frames;
+      // profiles/r03n_flow_stamps_batch.txt), so bigger batches are cut into
+      // balanced sub-batches.
+      const long tiles_frame = (long)g.wg_per_row * (rq1 - r0);
+      const long ring = (long)g.flow_slots * cu_count();
+      if (tiles_frame * p.nframes > ring && p.nframes > 1) {
+        const int per_max = (int)(ring / tiles_frame > 1 ? ring / tiles_frame : 1);
+        const int nl = (p.nframes + per_max - 1) / per_max;
+        const int per = (p.nframes + nl - 1) / nl;
+        for (int f0 = 0; f0 < p.nframes; f0 += per) {
+          SearchArgs q = frame_args(p, f0);
+          q.nframes = min(per, p.nframes - f0);
+          q.ref_fstride = p.ref_fstride;
+          q.cur_fstride = p.cur_fstride;
+          q.ref_bytes = (uint32_t)((q.nframes - 1) * p.ref_fstride + p.ref_bytes1);
+          q.cur_bytes = (uint32_t)((q.nframes - 1) * p.cur_fstride + p.cur_bytes1);
+          const hipError_t e = launch_search(q, stream, used_fast);
+          if (e != hipSuccess) return e;
+        }
+        return hipSuccess;
+      }
+      SearchArgs q = p;
+      hipError_t e = hipSuccess;
+      if (rq1 > r0) {
+        q.block_row_end = rq1;  // the flow kernel's rows; records keep p's frame stride
+        e = launch_flow(q, g, r0, rq1 - r0, stream);
+        if (e != hipSuccess) return e;
+      }
+      if (used_fast) *used_fast = 3;
+      for (int f = 0; f < p.nframes; f++) {
+        const SearchArgs s = frame_args(p, f);
+        if (rq1 < r1 && (e = launch_generic(s, 0, g.nbx_full, rq1, r1 - rq1, stream)) != hipSuccess)
+          return e;
+        if (g.nbx_full < p.nbx &&
+            (e = launch_generic(s, g.nbx_full, p.nbx - g.nbx_full, r0, r1 - r0, stream)) != hipSuccess)
+          return e;
+      }
+      return hipSuccess;
+    }
+    for (int f = 0; f < p.nframes; f++) {
+      hipError_t e = launch_search(frame_args(p, f), stream, used_fast);
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+  }
   if (p.cost_kind == COST_SSIM) return launch_ssim(p, stream);
   MfmaGeom mg;
   if (p.cost_kind == COST_SSD && p.scratch && plan_mfma_ssd(p, &mg) &&

@@ -185,6 +185,41 @@ class Engine:
             cost_t.data_ptr() if cost_t is not None else None, st), self._h)
 
 
+    def search_batch_device(self, ref_t, ref_row0: int, cur_t, cur_row0: int, width: int,
+                            height: int, blk: int, span: int, cost, row_begin: int, row_end: int,
+                            mv_t, cost_t=None, stream=None, stride=None):
+        """A batch of stripes in one launch (me_full_search_batch_device):
+        ref_t / cur_t are uint8 tensors [F, rows, pitch] (frame f = ref_t[f]),
+        mv_t int16 [F * nblk, 2] and cost_t [F * nblk], frame-major."""
+        st = stream if stream is not None else _current_stream()
+        check(_lib.lib().me_full_search_batch_device(*self._batch_args(
+            ref_t, ref_row0, cur_t, cur_row0, width, height, blk, span, cost, row_begin, row_end,
+            mv_t, cost_t, st, stride)), self._h)
+
+    def _batch_args(self, ref_t, ref_row0, cur_t, cur_row0, width, height, blk, span, cost,
+                    row_begin, row_end, mv_t, cost_t, stream, stride):
+        if ref_t.dim() != 3 or cur_t.dim() != 3 or ref_t.shape[0] != cur_t.shape[0]:
+            raise MEError(_lib.ME_EINVAL, f"batch shapes {tuple(ref_t.shape)} / {tuple(cur_t.shape)}")
+        es = ref_t.element_size()
+        return (self._h, ref_t.data_ptr(), ref_t.stride(0) * es, ref_row0, cur_t.data_ptr(),
+                cur_t.stride(0) * es, cur_row0, width, height, stride or ref_t.stride(1) * es,
+                blk, span, cost_code(cost), row_begin, row_end, ref_t.shape[0],
+                mv_t.data_ptr(), cost_t.data_ptr() if cost_t is not None else None, stream)
+
+    def prepared_batch_search(self, ref_t, ref_row0, cur_t, cur_row0, width, height, blk, span,
+                              cost, row_begin, row_end, mv_t, cost_t, stream=None, stride=None):
+        """Zero-argument callable enqueueing search_batch_device(...) with these buffers."""
+        fn, h = _lib.lib().me_full_search_batch_device, self._h
+        args = self._batch_args(ref_t, ref_row0, cur_t, cur_row0, width, height, blk, span, cost,
+                                row_begin, row_end, mv_t, cost_t,
+                                stream if stream is not None else _current_stream(), stride)
+
+        def run():
+            s = fn(*args)
+            if s:
+                check(s, h)
+        return run
+
     # ---- multi-process stripes: the one exchange step in native code ----
     @staticmethod
     def comm_unique_id() -> bytes:

@@ -373,3 +373,66 @@ def test_stripes_of_multi_gpu_splits(engine, span):
                 np.testing.assert_array_equal(cot.cpu().numpy().view(np.uint32), ocost[b0:b1],
                                               err_msg=msg)
     engine.device_check()
+
+
+@pytest.mark.parametrize("cost,blk,span,w,h,ways", [
+    ("sad", 16, 32, 1920, 1080, 8),   # flow kernel, one launch for the batch (h = 8 bottom row)
+    ("sad", 16, 32, 1920, 1080, 1),   # whole frames batched
+    ("sad", 16, 16, 1000, 700, 3),    # partial right column + h = 12 bottom row: per-frame kernels
+    ("ssd", 16, 32, 1920, 1080, 4),   # matrix cores, frame by frame
+    ("sad", 8, 24, 640, 360, 2),      # 8x8 item kernel, frame by frame
+])
+def test_batch_search_equals_per_frame(engine, cost, blk, span, w, h, ways):
+    """me_full_search_batch_device: F stripes (or whole frames) of different
+    frames in one call equal the oracle frame by frame, with records laid out
+    frame-major; padded frame strides are honoured."""
+    import torch
+    from motionestimation_amd import shard
+    F = 3
+    base_ref, base_cur = synth.frame_pair(w, h, 31, 4, -3)
+    frames = [(np.roll(base_ref, 37 * f, axis=1), np.roll(base_cur, 37 * f, axis=1))
+              for f in range(F)]
+    oracle = [O.full_search(r, c, blk, span, cost, threads=NT)[:2] for r, c in frames]
+    for st in shard.plan(w, h, blk, span, ways):
+        if not st.nblocks:
+            continue
+        pad = 48  # frames further apart than their rows: strides are taken as given
+        rr, cr = st.ref_y1 - st.ref_y0, st.cur_y1 - st.cur_y0
+        ref_b = torch.zeros((F, rr + pad, w), dtype=torch.uint8, device="cuda")
+        cur_b = torch.zeros((F, cr + pad, w), dtype=torch.uint8, device="cuda")
+        for f, (r, c) in enumerate(frames):
+            ref_b[f, :rr] = torch.from_numpy(r[st.ref_y0:st.ref_y1].copy())
+            cur_b[f, :cr] = torch.from_numpy(c[st.cur_y0:st.cur_y1].copy())
+        mv = torch.full((F * st.nblocks, 2), -5, dtype=torch.int16, device="cuda")
+        co = torch.zeros(F * st.nblocks, dtype=torch.int32, device="cuda")
+        for _ in range(2):
+            engine.search_batch_device(ref_b, st.ref_y0, cur_b, st.cur_y0, w, h, blk, span, cost,
+                                       st.row_begin, st.row_end, mv, co)
+        torch.cuda.synchronize()
+        mv, co = mv.cpu().numpy(), co.cpu().numpy().view(np.uint32)
+        b0, b1 = st.row_begin * st.nbx, st.row_end * st.nbx
+        for f in range(F):
+            n = st.nblocks
+            msg = f"{cost} {w}x{h} B{blk} S{span} rows {st.row_begin}:{st.row_end} frame {f}"
+            np.testing.assert_array_equal(mv[f * n:(f + 1) * n], oracle[f][0][b0:b1], err_msg=msg)
+            np.testing.assert_array_equal(co[f * n:(f + 1) * n], oracle[f][1][b0:b1], err_msg=msg)
+    engine.device_check()
+
+
+def test_batch_search_argument_checks(engine):
+    import torch
+    L = me._lib.lib()
+    ref = torch.zeros((2, 64, 64), dtype=torch.uint8, device="cuda")
+    mv = torch.zeros((2 * 16, 2), dtype=torch.int16, device="cuda")
+    base = dict(ref_stride=64 * 64, cur_stride=64 * 64, n=2)
+
+    def call(ref_stride=base["ref_stride"], cur_stride=base["cur_stride"], n=base["n"]):
+        return L.me_full_search_batch_device(engine._h, ref.data_ptr(), ref_stride, 0,
+                                             ref.data_ptr(), cur_stride, 0, 64, 64, 64, 16, 8,
+                                             1, 0, 4, n, mv.data_ptr(), None, None)
+    assert call() == me._lib.ME_OK
+    assert call(ref_stride=64 * 63) == me._lib.ME_EINVAL   # frames would overlap
+    assert call(cur_stride=100) == me._lib.ME_EINVAL
+    assert call(n=0) == me._lib.ME_EINVAL
+    assert call(ref_stride=1 << 31) == me._lib.ME_EUNSUPPORTED
+    torch.cuda.synchronize()

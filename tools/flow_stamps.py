@@ -21,8 +21,22 @@ n = me.num_blocks(1920, 1080, 16)
 mv = torch.empty((n, 2), dtype=torch.int16, device="cuda")
 co = torch.empty(n, dtype=torch.int32, device="cuda")
 rows = sys.argv[1] if len(sys.argv) > 1 else ""
+if rows.startswith("batch"):  # batchF: F frames in one launch (me_full_search_batch_device)
+    F = int(rows[5:])
+    rows = ""
+    rb = torch.from_numpy(np.stack([ref] * F)).cuda()
+    cb = torch.from_numpy(np.stack([cur] * F)).cuda()
+    mvb = torch.empty((F * n, 2), dtype=torch.int16, device="cuda")
+    cob = torch.empty(F * n, dtype=torch.int32, device="cuda")
+    for _ in range(40):  # past the clock ramp (tools/dbg/ramp_probe.py)
+        eng.search_batch_device(rb, 0, cb, 0, 1920, 1080, 16, 32, "sad", 0, 68, mvb, cob)
+else:
+    for _ in range(400):  # past the clock ramp (tools/dbg/ramp_probe.py)
+        eng.full_search_device(rt, ct, 16, 32, "sad", mv, co)
 for _ in range(20):
-    if rows:
+    if "F" in dir() and not rows:
+        eng.search_batch_device(rb, 0, cb, 0, 1920, 1080, 16, 32, "sad", 0, 68, mvb, cob)
+    elif rows:
         a, b = (int(x) for x in rows.split(":"))
         eng.search_stripe_device(rt, 0, ct, 0, 1920, 1080, 16, 32, "sad", a, b, mv, co)
     else:

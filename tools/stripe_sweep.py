@@ -3,9 +3,10 @@
 For N in --ranks, plan the N candidate-balanced stripes (me_plan_stripes) of a
 BASELINE config and time every rank's stripe search (its halo-only planes,
 me_full_search_stripe_device) back to back on this GPU.  The slowest stripe is
-the compute-bound step time of the N-GPU strong-scaling run (the RCCL gather
-overlaps the next frame's search in bench.py's stripe mode), so
-t(N=1) / max_r t_r(N) is the compute-side speed-up ceiling.  One JSON line per N.
+the compute-bound step time of the N-GPU strong-scaling run (before the
+RCCL gather), so t(N=1) / max_r t_r(N) is the compute-side speed-up ceiling.
+--frames F times F frames' stripes per launch (the batched step of bench.py).
+One JSON line per N (times per launch, i.e. per F frames).
 
   python tools/stripe_sweep.py [--config 1080p|4k|8k] [--cost sad] [--ranks 1,2,4,8]
 """
@@ -14,6 +15,7 @@ import json
 import os
 import sys
 
+import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -30,11 +32,25 @@ def main():
     ap.add_argument("--cost", default="sad")
     ap.add_argument("--ranks", default="1,2,4,8")
     ap.add_argument("--iters", type=int, default=30)
+    ap.add_argument("--frames", type=int, default=1,
+                    help="frames per launch (me_full_search_batch_device): the batched step")
     a = ap.parse_args()
     cfg, blk, span = CONFIGS[a.config]
     w, h, seed, sx, sy = synth.CONFIGS[cfg]
     ref, cur = synth.frame_pair(w, h, seed, sx, sy)
     eng = me.Engine()
+    # GPU clock ramp (bench.clock_ramp): ~100 ms of whole-frame searches first,
+    # or the first (N = 1) line is timed on a rising clock
+    rt0, ct0 = torch.from_numpy(ref).cuda(), torch.from_numpy(cur).cuda()
+    nb0 = me.num_blocks(w, h, blk)
+    mv0 = torch.empty((nb0, 2), dtype=torch.int16, device="cuda")
+    co0 = torch.empty(nb0, dtype=torch.int32, device="cuda")
+    import time
+    t_end = time.perf_counter() + 0.1
+    while time.perf_counter() < t_end:
+        for _ in range(4):
+            eng.full_search_device(rt0, ct0, blk, span, a.cost, mv0, co0)
+        torch.cuda.synchronize()
     base = None
     for n in [int(x) for x in a.ranks.split(",")]:
         times = []
@@ -42,14 +58,17 @@ def main():
             if not st.nblocks:
                 times.append(0.0)
                 continue
-            rt = torch.from_numpy(ref[st.ref_y0:st.ref_y1].copy()).cuda()
-            ct = torch.from_numpy(cur[st.cur_y0:st.cur_y1].copy()).cuda()
-            mv = torch.empty((st.nblocks, 2), dtype=torch.int16, device="cuda")
-            co = torch.empty(st.nblocks, dtype=torch.int32, device="cuda")
+            F = a.frames
+            rt = torch.from_numpy(np.stack([np.roll(ref, 37 * f, axis=1)[st.ref_y0:st.ref_y1]
+                                            for f in range(F)])).cuda()
+            ct = torch.from_numpy(np.stack([np.roll(cur, 37 * f, axis=1)[st.cur_y0:st.cur_y1]
+                                            for f in range(F)])).cuda()
+            mv = torch.empty((F * st.nblocks, 2), dtype=torch.int16, device="cuda")
+            co = torch.empty(F * st.nblocks, dtype=torch.int32, device="cuda")
 
             def run():
-                eng.search_stripe_device(rt, st.ref_y0, ct, st.cur_y0, w, h, blk, span, a.cost,
-                                         st.row_begin, st.row_end, mv, co)
+                eng.search_batch_device(rt, st.ref_y0, ct, st.cur_y0, w, h, blk, span, a.cost,
+                                        st.row_begin, st.row_end, mv, co)
             for _ in range(5):
                 run()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -62,7 +81,7 @@ def main():
             times.append(e0.elapsed_time(e1) / a.iters)
         t = max(times)
         base = base or t
-        print(json.dumps({"config": a.config, "cost": a.cost, "ranks": n,
+        print(json.dumps({"config": a.config, "cost": a.cost, "ranks": n, "frames": a.frames,
                           "stripe_ms": [round(x, 4) for x in times], "max_ms": t,
                           "compute_speedup_vs_1": base / t}), flush=True)
 
