@@ -268,10 +268,10 @@ def batch_frames(ref, cur, nframes):
 class StripeRun:
     """F frames per step in row stripes over the ranks.
 
-    Rank r holds its cur stripe and the ref rows with the S-row halo of each of
-    the step's F frames, searches its block rows of all F in one launch
-    (me_full_search_batch_device), and sends its padded records to rank 0 in
-    one gather per step.  With RCCL the gather is the library's ncclGather,
+    Rank r holds, for each of the step's F frames, one stripe's cur rows and
+    ref rows with the S-row halo, searches all F stripes together
+    (me_search_stripes_device: one launch where the kernels allow), and sends
+    its padded records to rank 0 in one gather per step.  With RCCL the gather is the library's ncclGather,
     enqueued right after the search on the same stream: the host never waits
     inside the timed region."""
 
@@ -284,12 +284,23 @@ class StripeRun:
         self.eng, self.dev, self.world, self.rank, self.gloo = eng, dev, world, rank, gloo
         self.w, self.h, self.blk, self.span, self.cost, self.nframes = w, h, blk, span, cost, F
         self.stripes = shard.plan(w, h, blk, span, world)
-        self.st = st = self.stripes[rank]
-        self.ref_t = torch.from_numpy(np.stack([r[st.ref_y0:st.ref_y1] for r, _ in frames])).to(dev)
-        self.cur_t = torch.from_numpy(np.stack([c[st.cur_y0:st.cur_y1] for _, c in frames])).to(dev)
-        # records: frame f's stripe at [f * nblocks, (f + 1) * nblocks), padded to F * max_blocks
-        self.recs = [torch.zeros((2, F * st.max_blocks), dtype=torch.int32, device=dev)
-                     for _ in range(2)]
+        # Rank r searches stripe (r + f) % N of frame f: over N frames every
+        # rank holds every stripe once, so the ranks' rows balance exactly
+        # (an 8-way 1080p split has 9- and 8-row stripes: 9-row ranks took
+        # 92.8 us per 8 frames against 78.5, profiles/r03o_*).
+        self.own = [self.stripes[(rank + f) % world] for f in range(F)]
+        self.st = self.own[0]
+        mb = self.stripes[0].max_blocks
+        ref_rows = max(st.ref_y1 - st.ref_y0 for st in self.own)
+        cur_rows = max(st.cur_y1 - st.cur_y0 for st in self.own)
+        self.ref_t = torch.zeros((F, ref_rows, w), dtype=torch.uint8, device=dev)
+        self.cur_t = torch.zeros((F, cur_rows, w), dtype=torch.uint8, device=dev)
+        for f, ((r, c), st) in enumerate(zip(frames, self.own)):
+            self.ref_t[f, :st.ref_y1 - st.ref_y0] = torch.from_numpy(r[st.ref_y0:st.ref_y1].copy())
+            self.cur_t[f, :st.cur_y1 - st.cur_y0] = torch.from_numpy(c[st.cur_y0:st.cur_y1].copy())
+        # records: frame f's stripe at [f * max_blocks, f * max_blocks + its nblocks)
+        self.recs = [torch.zeros((2, F * mb), dtype=torch.int32, device=dev) for _ in range(2)]
+        self.mb = mb
         cdev = torch.device("cpu") if gloo else dev
         self.i = 0
         # RCCL ranks gather in libme_hip (me_gather_device) on the search's own
@@ -302,11 +313,12 @@ class StripeRun:
         # (a one-rank RCCL group under torch.distributed.run takes this path too:
         # the GPU test of the library gather on a one-GPU box)
         self.lib = dist.is_initialized() and not gloo
-        mvs = [r[0].view(torch.int16).view(F * st.max_blocks, 2) for r in self.recs]
-        self.run_search = [eng.prepared_batch_search(
-            self.ref_t, st.ref_y0, self.cur_t, st.cur_y0, w, h, blk, span, cost, st.row_begin,
-            st.row_end, mvs[k], self.recs[k][1]) if st.nblocks else (lambda: None)
-            for k in range(2)]
+        mvs = [r[0].view(torch.int16).view(F * mb, 2) for r in self.recs]
+        jobs = [[(self.ref_t[f], st.ref_y0, self.cur_t[f], st.cur_y0, st.row_begin, st.row_end,
+                  mvs[k][f * mb:], self.recs[k][1][f * mb:])
+                 for f, st in enumerate(self.own) if st.nblocks] for k in range(2)]
+        self.run_search = [eng.prepared_stripes_search(w, h, blk, span, cost, jobs[k], stride=w)
+                           if jobs[k] else (lambda: None) for k in range(2)]
         self.graphs = None
         if self.lib:
             if not eng.comm_ranks:  # one communicator per context (stripe_4k reuses it)
@@ -326,7 +338,7 @@ class StripeRun:
             # 20.6 vs 15.5 us; hipGraphLaunch's host time, profiles/r03a_step_overhead_graph.jsonl).
             # Each is run once uncaptured first: that sizes the search scratch
             # and sets up RCCL's connections.
-            if graph and st.nblocks:
+            if graph and jobs[0]:
                 from motionestimation_amd import MEError
                 stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
                 for k in range(2):
@@ -379,14 +391,13 @@ class StripeRun:
         if self.rank != 0:
             return None
         recs = [self.recs[k].cpu()] if self.world == 1 and not self.lib else self.bufs[k]
+        recs = [np.asarray(r.cpu() if hasattr(r, "cpu") else r) for r in recs]
         out = []
         for f in range(self.nframes):
-            per_rank = []
-            for st, rec in zip(self.stripes, recs):
-                rec = np.asarray(rec.cpu() if hasattr(rec, "cpu") else rec)
-                n = st.nblocks
-                per_rank.append(rec[:, f * n:(f + 1) * n])
-            out.append(shard.assemble(per_rank, self.stripes))
+            # stripe s of frame f: rank (s - f) mod N, record slot f
+            per_stripe = [recs[(s - f) % self.world][:, f * self.mb:f * self.mb + st.nblocks]
+                          for s, st in enumerate(self.stripes)]
+            out.append(shard.assemble(per_stripe, self.stripes))
         return out
 
 
@@ -628,7 +639,6 @@ def main():
         ref, cur = synth.frame_pair(w, h, seed, sx, sy)
         frames = batch_frames(ref, cur, F)
         sr = StripeRun(eng, dev, world, rank, gloo, frames, blk, span, args.cost, args.graph)
-        st = sr.st
         units_per_step = cands_frame * F
         elapsed, kern_ms = timed(sr.step, args.steps, args.warmup, world, ramp_ms=args.ramp_ms)
         parity = stripe_parity(eng, sr, frames, dev)
@@ -644,7 +654,8 @@ def main():
         alg_bytes = F * (2 * w * h + 8 * nb)
         absdiffs = F * exact_absdiffs(w, h, blk, span)
     else:
-        alg_bytes = F * ((st.ref_y1 - st.ref_y0 + st.cur_y1 - st.cur_y0) * w + 8 * st.nblocks)
+        alg_bytes = sum((o.ref_y1 - o.ref_y0 + o.cur_y1 - o.cur_y0) * w + 8 * o.nblocks
+                        for o in sr.own)
         absdiffs = F * exact_absdiffs(w, h, blk, span) / world
     achieved = alg_bytes / (kern_ms / 1e3) / 1e9
     tag = f"{args.config}_b{blk}_s{span}_{args.cost}"

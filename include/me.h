@@ -143,18 +143,34 @@ me_status me_full_search_stripe_device(me_ctx* ctx, const uint8_t* d_ref,
                                        int16_t* d_mv_xy, uint32_t* d_block_cost,
                                        void* stream);
 
-/* A batch of n_frames stripes (or whole frames: block rows [0, nby)) in one
- * launch.  Frame f's ref rows start at d_ref + f * ref_frame_stride bytes and
- * its cur rows at d_cur + f * cur_frame_stride; every frame has the geometry,
- * row pitch, block rows and resident-row contract of
- * me_full_search_stripe_device (ref_row0 / cur_row0 are the frame rows of each
- * frame's first resident row).  Frame f's records are written at
+/* Several stripes (of one frame or of several frames of the same geometry)
+ * searched together: each job is what one me_full_search_stripe_device call
+ * would take -- its planes with their first resident rows, its block rows and
+ * its output records -- and the results are those of one call per job.  The
+ * jobs of a call share launches where the kernels allow it, so a batch fills
+ * the GPU where one small stripe cannot: the per-rank step of a multi-GPU
+ * split over several frames (a rank may hold different row ranges of
+ * different frames, balancing its total rows).  Asynchronous on `stream`. */
+typedef struct me_stripe_job {
+  const uint8_t* d_ref;
+  int ref_row0;
+  const uint8_t* d_cur;
+  int cur_row0;
+  int block_row_begin, block_row_end;
+  int16_t* d_mv_xy;        /* (block_row_end - block_row_begin) * ceil(W/B) records */
+  uint32_t* d_block_cost;  /* may be NULL */
+} me_stripe_job;
+me_status me_search_stripes_device(me_ctx* ctx, int width, int height, int stride,
+                                   int block_size, int search_range, me_cost cost,
+                                   const me_stripe_job* jobs, int n_jobs, void* stream);
+
+/* A batch of n_frames same-shaped stripes (or whole frames: block rows
+ * [0, nby)): frame f's rows at d_ref + f * ref_frame_stride and
+ * d_cur + f * cur_frame_stride bytes (frames must not overlap), its records at
  * d_mv_xy + 2 * f * nblk and d_block_cost + f * nblk, nblk = (block_row_end -
- * block_row_begin) * ceil(W/B).  Results are those of one
- * me_full_search_stripe_device per frame; a batch fills the GPU where one small
- * stripe cannot (the per-rank step of a multi-GPU split over several frames:
- * one launch and one gather for all of them).  The whole batch stays below
- * 2 GiB per plane stack (ME_EUNSUPPORTED otherwise). */
+ * block_row_begin) * ceil(W/B).  The equal-stripes case of
+ * me_search_stripes_device.  Each plane stack of the batch stays below 2 GiB
+ * ((n_frames - 1) * stride + one frame's bytes; ME_EUNSUPPORTED otherwise). */
 me_status me_full_search_batch_device(me_ctx* ctx, const uint8_t* d_ref,
                                       size_t ref_frame_stride, int ref_row0,
                                       const uint8_t* d_cur, size_t cur_frame_stride,

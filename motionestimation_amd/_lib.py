@@ -45,6 +45,8 @@ _SIGS = {
                                                    ctypes.c_int, _u8p, ctypes.c_size_t] +
                                     [ctypes.c_int] * 10 +
                                     [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "me_search_stripes_device": (ctypes.c_int, [ctypes.c_void_p] + [ctypes.c_int] * 6 +
+                                 [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),  # jobs: me_stripe_job*
     "me_plan_stripes": (ctypes.c_int, [ctypes.c_int] * 5 + [ctypes.POINTER(ctypes.c_int)]),
     "me_comm_unique_id": (ctypes.c_int, [ctypes.c_void_p]),
     "me_comm_init": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),

@@ -159,11 +159,6 @@ SearchArgs make_args(const uint8_t* ref, int ref_row0, const uint8_t* cur, int c
   const long ref_rows = ref_end - ref_row0, cur_rows = cur_end - cur_row0;
   p.ref_bytes = ref_rows > 0 ? (uint32_t)((ref_rows - 1) * (long)stride + width) : 0;
   p.cur_bytes = cur_rows > 0 ? (uint32_t)((cur_rows - 1) * (long)stride + width) : 0;
-  p.ref_bytes1 = p.ref_bytes;
-  p.cur_bytes1 = p.cur_bytes;
-  p.nframes = 1;
-  p.ref_fstride = p.cur_fstride = 0;
-  p.out_fstride = (r1 - r0) * p.nbx;
   p.sched = nullptr;
   p.scratch = nullptr;
   p.scratch_bytes = 0;
@@ -654,41 +649,93 @@ me_status me_full_search_stripe_device(me_ctx* c, const uint8_t* d_ref, int ref_
   return launch_ordered(c, c->devs[0], p, (hipStream_t)stream);
 }
 
+me_status me_search_stripes_device(me_ctx* c, int width, int height, int stride, int blk,
+                                   int range, me_cost cost, const me_stripe_job* jobs, int n_jobs,
+                                   void* stream) {
+  if (!c) return ME_EINVAL;
+  if (!jobs || n_jobs < 0) return fail(c, ME_EINVAL, "job list");
+  if (n_jobs == 0) return ME_OK;
+  const int nby = blk > 0 ? (height + blk - 1) / blk : 0;
+  std::vector<me::SearchJob> js((size_t)n_jobs);
+  me::SearchArgs base{};
+  Dev& d = c->devs[0];
+  const bool cap = me::capturing((hipStream_t)stream);
+  for (int i = 0; i < n_jobs; i++) {
+    const me_stripe_job& J = jobs[i];
+    me_status s = check_args(c, J.d_ref, J.d_cur, width, height, stride, blk, range, cost,
+                             J.d_mv_xy);
+    if (s != ME_OK) return s;
+    const int r0 = J.block_row_begin, r1 = J.block_row_end;
+    if (r0 < 0 || r1 > nby || r0 > r1)
+      return fail(c, ME_EINVAL, "job %d: block rows [%d, %d)", i, r0, r1);
+    const int need_ref0 = r0 * blk - range > 0 ? r0 * blk - range : 0;
+    if (J.ref_row0 < 0 || J.ref_row0 > need_ref0)
+      return fail(c, ME_EINVAL, "job %d: ref_row0 %d", i, J.ref_row0);
+    if (J.cur_row0 < 0 || J.cur_row0 > r0 * blk)
+      return fail(c, ME_EINVAL, "job %d: cur_row0 %d", i, J.cur_row0);
+    js[i] = me::SearchJob{J.d_ref, J.ref_row0, J.d_cur, J.cur_row0, r0, r1, J.d_mv_xy, J.d_block_cost};
+    // grow the device scratch to the largest job (the MFMA SSD path runs job by job)
+    me::SearchArgs p = make_args(J.d_ref, J.ref_row0, J.d_cur, J.cur_row0, width, height, stride,
+                                 blk, range, cost, r0, r1, J.d_mv_xy, J.d_block_cost);
+    if ((s = attach_scratch(c, d, p, cap)) != ME_OK) return s;
+  }
+  // geometry, cost and the (final) scratch buffers every job's launch takes
+  base = make_args(jobs[0].d_ref, jobs[0].ref_row0, jobs[0].d_cur, jobs[0].cur_row0, width, height,
+                   stride, blk, range, cost, jobs[0].block_row_begin, jobs[0].block_row_end,
+                   jobs[0].d_mv_xy, jobs[0].d_block_cost);
+  {
+    me_status s = attach_scratch(c, d, base, cap);
+    if (s != ME_OK) return s;
+  }
+  c->err[0] = 0;
+  if (!cap) {
+    me_status s = me::order_on(c, d, (hipStream_t)stream);
+    if (s != ME_OK) return s;
+  }
+  const hipError_t e = me::launch_jobs(base, js.data(), n_jobs, (hipStream_t)stream);
+  if (e != hipSuccess) {
+    if (!cap) {
+      (void)hipMemsetAsync(d.sched, 0, 64, (hipStream_t)stream);
+      if (d.mkeys) (void)hipMemsetAsync(d.mkeys, 0xFF, d.merge_cap * 16 * 8, (hipStream_t)stream);
+      if (d.mcnt) (void)hipMemsetAsync(d.mcnt, 0, d.merge_cap * 4, (hipStream_t)stream);
+    }
+    return fail(c, ME_EDEVICE, "search launch: %s", hipGetErrorString(e));
+  }
+  return ME_OK;
+}
+
 me_status me_full_search_batch_device(me_ctx* c, const uint8_t* d_ref, size_t ref_frame_stride,
                                      int ref_row0, const uint8_t* d_cur, size_t cur_frame_stride,
                                      int cur_row0, int width, int height, int stride, int blk,
                                      int range, me_cost cost, int r0, int r1, int n_frames,
                                      int16_t* d_mv, uint32_t* d_cost, void* stream) {
+  if (!c) return ME_EINVAL;
+  if (n_frames < 1 || n_frames > 4096) return fail(c, ME_EINVAL, "n_frames %d", n_frames);
   me_status s = check_args(c, d_ref, d_cur, width, height, stride, blk, range, cost, d_mv);
   if (s != ME_OK) return s;
   const int nby = (height + blk - 1) / blk;
   if (r0 < 0 || r1 > nby || r0 > r1) return fail(c, ME_EINVAL, "block rows [%d, %d)", r0, r1);
-  if (n_frames < 1) return fail(c, ME_EINVAL, "n_frames %d", n_frames);
-  const int need_ref0 = r0 * blk - range > 0 ? r0 * blk - range : 0;
-  if (ref_row0 < 0 || ref_row0 > need_ref0) return fail(c, ME_EINVAL, "ref_row0 %d", ref_row0);
-  if (cur_row0 < 0 || cur_row0 > r0 * blk) return fail(c, ME_EINVAL, "cur_row0 %d", cur_row0);
-  c->err[0] = 0;
-  me::SearchArgs p = make_args(d_ref, ref_row0, d_cur, cur_row0, width, height, stride, blk,
-                               range, cost, r0, r1, d_mv, d_cost);
-  if (n_frames > 1) {
-    // every frame's resident rows inside its stride; the batch addressable
-    // with 32-bit offsets (buffer descriptors)
-    if (ref_frame_stride < p.ref_bytes1 || cur_frame_stride < p.cur_bytes1)
-      return fail(c, ME_EINVAL, "frame strides %zu / %zu below a frame's %u / %u bytes",
-                  ref_frame_stride, cur_frame_stride, p.ref_bytes1, p.cur_bytes1);
-    const unsigned long long rb = (unsigned long long)(n_frames - 1) * ref_frame_stride + p.ref_bytes1;
-    const unsigned long long cb = (unsigned long long)(n_frames - 1) * cur_frame_stride + p.cur_bytes1;
-    if (rb >= (1ull << 31) || cb >= (1ull << 31))
-      return fail(c, ME_EUNSUPPORTED, "batch of %llu / %llu bytes (limit 2 GiB)", rb, cb);
-    p.nframes = n_frames;
-    p.ref_fstride = (uint32_t)ref_frame_stride;
-    p.cur_fstride = (uint32_t)cur_frame_stride;
-    p.ref_bytes = (uint32_t)rb;
-    p.cur_bytes = (uint32_t)cb;
-  }
-  const bool cap = me::capturing((hipStream_t)stream);
-  if ((s = attach_scratch(c, c->devs[0], p, cap)) != ME_OK) return s;
-  return launch_ordered(c, c->devs[0], p, (hipStream_t)stream);
+  // every frame's resident rows inside its stride (frames must not overlap)
+  const me::SearchArgs p = make_args(d_ref, ref_row0, d_cur, cur_row0, width, height, stride, blk,
+                                     range, cost, r0, r1, d_mv, d_cost);
+  if (n_frames > 1 && (ref_frame_stride < p.ref_bytes || cur_frame_stride < p.cur_bytes))
+    return fail(c, ME_EINVAL, "frame strides %zu / %zu below a frame's %u / %u bytes",
+                ref_frame_stride, cur_frame_stride, p.ref_bytes, p.cur_bytes);
+  // One plane stack per batch, below 2 GiB like a single plane (check_args):
+  // a stride past it is a caller error, refused before any frame address is
+  // formed (a wild stride would otherwise send the kernels to unmapped memory).
+  const unsigned long long rb = (unsigned long long)(n_frames - 1) * ref_frame_stride + p.ref_bytes;
+  const unsigned long long cb = (unsigned long long)(n_frames - 1) * cur_frame_stride + p.cur_bytes;
+  if (rb >= (1ull << 31) || cb >= (1ull << 31))
+    return fail(c, ME_EUNSUPPORTED, "batch of %llu / %llu bytes (limit 2 GiB)", rb, cb);
+  const size_t nblk = (size_t)(r1 - r0) * ((width + blk - 1) / blk);
+  std::vector<me_stripe_job> jobs((size_t)n_frames);
+  for (int f = 0; f < n_frames; f++)
+    jobs[f] = me_stripe_job{d_ref + (size_t)f * ref_frame_stride, ref_row0,
+                            d_cur + (size_t)f * cur_frame_stride, cur_row0, r0, r1,
+                            d_mv + 2 * (size_t)f * nblk, d_cost ? d_cost + (size_t)f * nblk : nullptr};
+  return me_search_stripes_device(c, width, height, stride, blk, range, cost, jobs.data(),
+                                  n_frames, stream);
 }
 
 me_status me_full_search_device(me_ctx* c, const uint8_t* d_ref, const uint8_t* d_cur,

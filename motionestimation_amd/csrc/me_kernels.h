@@ -31,14 +31,6 @@ struct SearchArgs {
   uint32_t* cost;
   uint32_t ref_bytes;  // readable bytes from ref (buffer range check), and from cur
   uint32_t cur_bytes;
-  // Batch of nframes frames (me_full_search_batch_device): frame f's planes
-  // start f * ref_fstride / cur_fstride bytes after ref / cur, its records
-  // f * out_fstride blocks after mv / cost; ref_bytes / cur_bytes cover the
-  // whole batch, ref_bytes1 / cur_bytes1 one frame.  nframes = 1 otherwise.
-  int nframes;
-  uint32_t ref_fstride, cur_fstride;
-  int out_fstride;
-  uint32_t ref_bytes1, cur_bytes1;
   uint32_t* sched;     // 16 u32: [0, 9) zeroed tile counters + arrivals (8 XCD groups),
                        // [SCHED_ERR] the invariant word; or null
   uint8_t* scratch;    // device scratch of the MFMA SSD path (mfma_ssd_scratch bytes) or null
@@ -74,6 +66,40 @@ struct QsadGeom {
   int flow_slots;  // me_flow_kernel: LDS ring slots (0: the persistent item kernel)
   int prio;        // waves issuing staging raise their issue priority (s_setprio) meanwhile
 };
+
+// A search job: block rows [r0, r1) of one frame (or row stripe), its planes
+// (ref / cur hold frame rows from ref_row0 / cur_row0, as in SearchArgs) and
+// its records (indexed from r0).  Jobs of one launch share the frame geometry.
+struct SearchJob {
+  const uint8_t* ref;
+  int ref_row0;
+  const uint8_t* cur;
+  int cur_row0;
+  int r0, r1;
+  int16_t* mv;
+  uint32_t* cost;
+};
+
+// The flow kernel's job table (kernel argument): job j owns launch tiles
+// [tile_pre[j], tile_pre[j + 1]).  A batch of frames or stripes (the per-rank
+// step of a multi-GPU split) fills the GPU in one launch.
+constexpr int MAX_JOBS = 16;
+struct FlowJobs {
+  int n;
+  int tile_pre[MAX_JOBS + 1];
+  int r0[MAX_JOBS];
+  int ref_row0[MAX_JOBS], cur_row0[MAX_JOBS];
+  uint32_t ref_bytes[MAX_JOBS], cur_bytes[MAX_JOBS];
+  const uint8_t* ref[MAX_JOBS];
+  const uint8_t* cur[MAX_JOBS];
+  int16_t* mv[MAX_JOBS];
+  uint32_t* cost[MAX_JOBS];
+};
+
+// Search every job (geometry, cost and scratch from base): SAD jobs the flow
+// kernel takes share launches (at most one LDS ring of tiles per CU each),
+// everything else runs job by job through launch_search.
+hipError_t launch_jobs(const SearchArgs& base, const SearchJob* jobs, int n, hipStream_t stream);
 
 // Matrix-core SSD path (me_mfma.hip): B = 16, full-height rows [row0, row0 +
 // nrows) x full-width columns [0, nbx); 4x4-block tiles.

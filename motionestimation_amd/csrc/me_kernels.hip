@@ -475,24 +475,17 @@ __device__ __forceinline__ void dma4(__amdgpu_buffer_rsrc_t rs, uint8_t* lds_dst
   }
 }
 
-// Geometry of one work item = (tile of TB blocks, dy pass); in a batched
-// launch (p.nframes > 1, the flow kernel) tiles run frame-major and f is the
-// item's frame: its planes start f * p.ref_fstride / cur_fstride bytes on and
-// its records f * p.out_fstride blocks on.
+// Geometry of one work item = (tile of TB blocks, dy pass); j: the flow
+// kernel's job (FlowJobs) the tile belongs to.
 struct Item {
-  int bx0, by, nb, tly, h, a, X0, c0, nch, prow0, prows, f;
+  int bx0, by, nb, tly, h, a, X0, c0, nch, prow0, prows, j;
 };
 
 template <int B, int K>
 __device__ __forceinline__ Item item_of(const SearchArgs& p, const QsadGeom& g, int tile,
                                         int pass) {
   Item it;
-  it.f = 0;
-  if (p.nframes > 1) {
-    const int tpf = g.wg_per_row * g.nrows;  // tiles per frame
-    it.f = tile / tpf;
-    tile -= it.f * tpf;
-  }
+  it.j = 0;
   it.bx0 = (tile % g.wg_per_row) * g.tb;
   it.by = g.row0 + tile / g.wg_per_row;
   it.nb = min(g.tb, g.nbx_full - it.bx0);
@@ -855,17 +848,36 @@ struct FlowCtl {
   uint32_t done[16];   // wave-tasks of the slot's item finished
 };
 
-// Single-wave LDS DMA of one item (the aligned path): tile rows and cur blocks.
+// Tile of the flow kernel's launch -> (job, tile of that job's rows): jobs
+// are consecutive tile ranges (jb.tile_pre), every job the same frame
+// geometry; a job's planes and records are its own.
+template <int B, int K>
+__device__ __forceinline__ Item flow_item(const SearchArgs& p, const QsadGeom& g,
+                                          const FlowJobs& jb, int tile) {
+  int j = 0;
+  while (j + 1 < jb.n && jb.tile_pre[j + 1] <= tile) j++;
+  QsadGeom gj = g;
+  gj.row0 = jb.r0[j];
+  Item it = item_of<B, K>(p, gj, tile - jb.tile_pre[j], 0);
+  it.j = j;
+  return it;
+}
+
+// Single-wave LDS DMA of one flow item (the aligned path): tile rows and cur
+// blocks, from its job's planes.
 template <int B>
 __device__ __forceinline__ void stage_item_wave(const SearchArgs& p, const QsadGeom& g, const Item& it,
-                                                uint8_t* buf, __amdgpu_buffer_rsrc_t rref,
-                                                __amdgpu_buffer_rsrc_t rcur) {
+                                                uint8_t* buf, const FlowJobs& jb) {
+  const __amdgpu_buffer_rsrc_t rref =
+      __builtin_amdgcn_make_buffer_rsrc((void*)jb.ref[it.j], (short)0, jb.ref_bytes[it.j], 0x00020000);
+  const __amdgpu_buffer_rsrc_t rcur =
+      __builtin_amdgcn_make_buffer_rsrc((void*)jb.cur[it.j], (short)0, jb.cur_bytes[it.j], 0x00020000);
   // lane recomputed per call (fresh_tid): hoisted lane-derived offsets spilled
   const int lane = fresh_tid() & 63;
   uint8_t* tile = buf;
   uint8_t* cur = buf + g.tile_bytes;
   const int pitch = g.pitch, stride = p.stride;
-  const uint32_t base = (uint32_t)it.f * p.ref_fstride + (uint32_t)((it.prow0 - p.ref_row0) * stride + it.X0);
+  const uint32_t base = (uint32_t)((it.prow0 - jb.ref_row0[it.j]) * stride + it.X0);
   const int bytes = it.prows * pitch;
   for (int s0 = 0; s0 < bytes; s0 += 1024) {  // 16-byte granules (g.tile16)
     const int d = s0 + 16 * lane;
@@ -875,7 +887,7 @@ __device__ __forceinline__ void stage_item_wave(const SearchArgs& p, const QsadG
           rref, (__attribute__((address_space(3))) void*)(tile + s0), 16,
           base + (uint32_t)(r * stride + x), 0, 0, 0);
   }
-  const uint32_t cbase = (uint32_t)it.f * p.cur_fstride + (uint32_t)((it.tly - p.cur_row0) * stride + it.bx0 * B);
+  const uint32_t cbase = (uint32_t)((it.tly - jb.cur_row0[it.j]) * stride + it.bx0 * B);
   const int cb = it.nb * B * B;
   for (int s0 = 0; s0 < cb; s0 += 1024) {
     const int d = s0 + 16 * lane;
@@ -898,7 +910,7 @@ __device__ __forceinline__ int flow_tasks(const SearchArgs& p, const QsadGeom& g
 }
 
 template <int B, int K, int PC>
-__global__ __launch_bounds__(1024) void me_flow_kernel(SearchArgs p, QsadGeom g) {
+__global__ __launch_bounds__(1024) void me_flow_kernel(SearchArgs p, QsadGeom g, FlowJobs jb) {
   static_assert(B == 16, "cur-block DMA layout of stage_item_wave");
   constexpr int CW = B / 4;
   extern __shared__ __align__(16) uint8_t smem[];
@@ -909,14 +921,10 @@ __global__ __launch_bounds__(1024) void me_flow_kernel(SearchArgs p, QsadGeom g)
   const int tid = (int)threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int S = p.range;
-  const __amdgpu_buffer_rsrc_t rref =
-      __builtin_amdgcn_make_buffer_rsrc((void*)p.ref, (short)0, p.ref_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rcur =
-      __builtin_amdgcn_make_buffer_rsrc((void*)p.cur, (short)0, p.cur_bytes, 0x00020000);
 
   // This workgroup's tiles: the XCD band of bid % 8 (a speed heuristic only),
-  // member m takes tiles band0 + m, + n_x, ... (all frames of a batch, frame-major)
-  const int ntiles = g.wg_per_row * g.nrows * p.nframes;
+  // member m takes tiles band0 + m, + n_x, ... (every job's tiles, job-major)
+  const int ntiles = jb.tile_pre[jb.n];
   const int nwg = (int)gridDim.x, bid = (int)blockIdx.x;
   const int ng = nwg < 8 ? nwg : 8;
   const int x = bid % ng, m = bid / ng;
@@ -943,8 +951,7 @@ __global__ __launch_bounds__(1024) void me_flow_kernel(SearchArgs p, QsadGeom g)
     // profiles/r02ae_ab_flow_start.txt).
     for (int i = 0; i < wave; i++) __builtin_amdgcn_s_sleep(10);
     if (g.prio) __builtin_amdgcn_s_setprio(3);  // see me_fast_kernel
-    stage_item_wave<B>(p, g, item_of<B, K>(p, g, tile_of(wave), 0), smem + wave * slot_bytes, rref,
-                       rcur);
+    stage_item_wave<B>(p, g, flow_item<B, K>(p, g, jb, tile_of(wave)), smem + wave * slot_bytes, jb);
     if (g.prio) __builtin_amdgcn_s_setprio(0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0)
@@ -968,7 +975,7 @@ __global__ __launch_bounds__(1024) void me_flow_kernel(SearchArgs p, QsadGeom g)
     q = (uint32_t)__builtin_amdgcn_readfirstlane((int)q);
     // advance to the item holding task q (pulls are in order: kc only grows)
     if (!have && kc < nitems) {
-      itc = item_of<B, K>(p, g, tile_of(kc), 0);
+      itc = flow_item<B, K>(p, g, jb, tile_of(kc));
       nwc = flow_tasks<B, K>(p, g, itc, &lc0c);
       have = true;
     }
@@ -976,7 +983,7 @@ __global__ __launch_bounds__(1024) void me_flow_kernel(SearchArgs p, QsadGeom g)
       basec += nwc;
       kc++;
       if (kc < nitems) {
-        itc = item_of<B, K>(p, g, tile_of(kc), 0);
+        itc = flow_item<B, K>(p, g, jb, tile_of(kc));
         nwc = flow_tasks<B, K>(p, g, itc, &lc0c);
       }
     }
@@ -1090,16 +1097,17 @@ __global__ __launch_bounds__(1024) void me_flow_kernel(SearchArgs p, QsadGeom g)
       if (lane < it.nb) {
         const uint64_t kk = keys[slot * g.tb + lane];
         keys[slot * g.tb + lane] = ~0ull;
-        const int out = it.f * p.out_fstride + (it.by - p.block_row_begin) * p.nbx + it.bx0 + lane;
-        p.mv[2 * out] = (int16_t)((int)(kk & 0xFFFF) - 32768);
-        p.mv[2 * out + 1] = (int16_t)((int)((kk >> 16) & 0xFFFF) - 32768);
-        if (p.cost) p.cost[out] = (uint32_t)(kk >> 32);
+        const int out = (it.by - jb.r0[it.j]) * p.nbx + it.bx0 + lane;
+        int16_t* mv = jb.mv[it.j];
+        mv[2 * out] = (int16_t)((int)(kk & 0xFFFF) - 32768);
+        mv[2 * out + 1] = (int16_t)((int)((kk >> 16) & 0xFFFF) - 32768);
+        if (jb.cost[it.j]) jb.cost[it.j][out] = (uint32_t)(kk >> 32);
       }
       if (lane == 0) __hip_atomic_store(&ctl->done[slot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       const int kn = kc + NB;
       if (kn < nitems) {
         if (g.prio) __builtin_amdgcn_s_setprio(3);
-        stage_item_wave<B>(p, g, item_of<B, K>(p, g, tile_of(kn), 0), buf, rref, rcur);
+        stage_item_wave<B>(p, g, flow_item<B, K>(p, g, jb, tile_of(kn)), buf, jb);
         if (g.prio) __builtin_amdgcn_s_setprio(0);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane == 0)
@@ -1360,11 +1368,10 @@ bool plan_flow(const SearchArgs& p, QsadGeom* g) {
   if (S < 16 || S % 16 || S > 32) return false;
   if (tuning().flow == 0) return false;
   const int nbx_full = p.width / B;
-  if (nbx_full < 1 || p.width % 16 || p.stride % 16 || (uintptr_t)p.ref % 16 || (uintptr_t)p.cur % 16 ||
-      p.ref_fstride % 16 || p.cur_fstride % 16)
+  if (nbx_full < 1 || p.width % 16 || p.stride % 16 || (uintptr_t)p.ref % 16 || (uintptr_t)p.cur % 16)
     return false;
   const int D = 2 * S + 1, G = S / 2;
-  const int rows = (p.block_row_end - p.block_row_begin) * p.nframes;  // every frame of a batch
+  const int rows = p.block_row_end - p.block_row_begin;  // launch_jobs: every job's rows
   const int cus = cu_count();
   auto pitch_of = [&](int tb) {
     int pt = ((tb - 1) * B + 4 * G + B + 4 + 15) & ~15;
@@ -1556,11 +1563,9 @@ hipError_t launch_fast(const SearchArgs& p, QsadGeom g, int K, int row0, int nro
 // them) so a steady stream of same-shape searches pays the planner once.
 struct PlanKey {
   int width, height, stride, blk, range, cost, rows, aligned;  // aligned: 1 (4 B) | 2 (16 B)
-  int nframes = 1;
   bool operator==(const PlanKey& o) const {
     return width == o.width && height == o.height && stride == o.stride && blk == o.blk &&
-           range == o.range && cost == o.cost && rows == o.rows && aligned == o.aligned &&
-           nframes == o.nframes;
+           range == o.range && cost == o.cost && rows == o.rows && aligned == o.aligned;
   }
 };
 struct PlanEntry {
@@ -1604,11 +1609,9 @@ static bool cached_flow_plan(const SearchArgs& p, QsadGeom* g) {
   static int used = 0, next = 0;
   static std::mutex mu;
   const int aligned = ((p.stride % 16 == 0) && ((uintptr_t)p.ref % 16 == 0) &&
-                       ((uintptr_t)p.cur % 16 == 0) && (p.ref_fstride % 16 == 0) &&
-                       (p.cur_fstride % 16 == 0)) ? 3 : 0;
-  PlanKey key{p.width, p.height, p.stride, p.blk, p.range, p.cost_kind,
-              p.block_row_end - p.block_row_begin, aligned};
-  key.nframes = p.nframes;
+                       ((uintptr_t)p.cur % 16 == 0)) ? 3 : 0;
+  const PlanKey key{p.width, p.height, p.stride, p.blk, p.range, p.cost_kind,
+                    p.block_row_end - p.block_row_begin, aligned};
   std::lock_guard<std::mutex> lk(mu);
   for (int i = 0; i < used; i++)
     if (cache[i].key == key) {
@@ -1626,12 +1629,35 @@ static bool cached_flow_plan(const SearchArgs& p, QsadGeom* g) {
   return e.ok;
 }
 
-static hipError_t launch_flow(const SearchArgs& p, QsadGeom g, int row0, int nrows,
+// One flow-kernel launch over jobs [0, n) (full-height rows and h = B/2
+// bottom rows only; n <= MAX_JOBS).
+static hipError_t launch_flow(const SearchArgs& p, QsadGeom g, const SearchJob* jobs, int n,
                               hipStream_t stream) {
-  if (nrows <= 0) return hipSuccess;
-  g.row0 = row0;
-  g.nrows = nrows;
-  const int ntiles = g.wg_per_row * nrows;
+  FlowJobs jb;
+  jb.n = 0;
+  jb.tile_pre[0] = 0;
+  const int B = p.blk, S = p.range, H = p.height;
+  for (int i = 0; i < n; i++) {
+    const SearchJob& J = jobs[i];
+    if (J.r1 <= J.r0) continue;
+    const int j = jb.n++;
+    jb.r0[j] = J.r0;
+    jb.ref_row0[j] = J.ref_row0;
+    jb.cur_row0[j] = J.cur_row0;
+    // bytes the job's descriptors may read: its resident rows (include/me.h)
+    const int ref_end = J.r1 * B + S < H ? J.r1 * B + S : H, cur_end = J.r1 * B < H ? J.r1 * B : H;
+    jb.ref_bytes[j] = (uint32_t)((long)(ref_end - J.ref_row0 - 1) * p.stride + p.width);
+    jb.cur_bytes[j] = (uint32_t)((long)(cur_end - J.cur_row0 - 1) * p.stride + p.width);
+    jb.ref[j] = J.ref;
+    jb.cur[j] = J.cur;
+    jb.mv[j] = J.mv;
+    jb.cost[j] = J.cost;
+    jb.tile_pre[j + 1] = jb.tile_pre[j] + g.wg_per_row * (J.r1 - J.r0);
+  }
+  const int ntiles = jb.tile_pre[jb.n];
+  if (ntiles <= 0) return hipSuccess;
+  g.row0 = 0;
+  g.nrows = 0;  // per job (jb.r0)
   const int nwg = ntiles > cu_count() ? cu_count() : ntiles;  // one per CU, at most one per tile
   // 144: the pitch of the 4-block tiles 1080p +-32 gets (row addresses in
   // the ds_read2 offsets); any other pitch takes the runtime-pitch body
@@ -1640,7 +1666,7 @@ static hipError_t launch_flow(const SearchArgs& p, QsadGeom g, int row0, int nro
     const hipError_t e = lds_attr((const void*)me_flow_kernel<16, 13, PP>, g.lds);              \
     if (e != hipSuccess) return e;                                                              \
     hipLaunchKernelGGL((me_flow_kernel<16, 13, PP>), dim3((unsigned)nwg), dim3(1024), g.lds,    \
-                       stream, p, g);                                                           \
+                       stream, p, g, jb);                                                       \
     return hipGetLastError();                                                                   \
   }
   ME_FLOW_CASE(144) ME_FLOW_CASE(0)
@@ -1653,36 +1679,40 @@ size_t merge_tiles_needed(const SearchArgs& p) {
   return p.cost_kind == COST_SSD ? mfma_merge_tiles(p) : 0;
 }
 
-static hipError_t launch_valu(const SearchArgs& p, hipStream_t stream, int* used_fast) {
-  const int r0 = p.block_row_begin, r1 = p.block_row_end;
-  if (r1 <= r0) return hipSuccess;
-  QsadGeom g;
-  int K = 0;
-  if (cached_flow_plan(p, &g)) {
-    // the flow kernel, like the item kernel, takes full-height rows and an
-    // h = B/2 bottom row; other partial bottom rows and the partial right
-    // column go to the generic kernel
-    const int nby = (p.height + p.blk - 1) / p.blk;
-    const int h_last = p.height - (nby - 1) * p.blk;
-    int rq1 = r1;
-    if (r1 == nby && h_last != p.blk && h_last != p.blk / 2) rq1 = r1 - 1;
-    hipError_t e = launch_flow(p, g, r0, rq1 - r0, stream);
-    if (e != hipSuccess) return e;
-    if (used_fast) *used_fast = 3;
-    if (rq1 < r1) {
-      e = launch_generic(p, 0, g.nbx_full, rq1, r1 - rq1, stream);
-      if (e != hipSuccess) return e;
-    }
-    if (g.nbx_full < p.nbx) return launch_generic(p, g.nbx_full, p.nbx - g.nbx_full, r0, r1 - r0, stream);
-    return hipSuccess;
-  }
-  if (!cached_plan(p, &g, &K)) return launch_generic(p, 0, p.nbx, r0, r1 - r0, stream);
-  // The qsad body is instantiated for full-height blocks and for h = B/2 (the
-  // 1080p bottom row); any other partial bottom row goes to the generic kernel.
+// The single-job arguments of job J (geometry, cost and scratch from base).
+static SearchArgs job_args(const SearchArgs& base, const SearchJob& J) {
+  SearchArgs q = base;
+  q.ref = J.ref;
+  q.ref_row0 = J.ref_row0;
+  q.cur = J.cur;
+  q.cur_row0 = J.cur_row0;
+  q.block_row_begin = J.r0;
+  q.block_row_end = J.r1;
+  q.mv = J.mv;
+  q.cost = J.cost;
+  const int B = base.blk, S = base.range, H = base.height;
+  const int ref_end = J.r1 * B + S < H ? J.r1 * B + S : H, cur_end = J.r1 * B < H ? J.r1 * B : H;
+  const long ref_rows = ref_end - J.ref_row0, cur_rows = cur_end - J.cur_row0;
+  q.ref_bytes = ref_rows > 0 ? (uint32_t)((ref_rows - 1) * (long)base.stride + base.width) : 0;
+  q.cur_bytes = cur_rows > 0 ? (uint32_t)((cur_rows - 1) * (long)base.stride + base.width) : 0;
+  return q;
+}
+
+// End of the full-height (and h = B/2) rows of [.., r1) the qsad bodies take;
+// a bottom row of another height goes to the generic kernel.
+static int qsad_rows_end(const SearchArgs& p, int r1) {
   const int nby = (p.height + p.blk - 1) / p.blk;
   const int h_last = p.height - (nby - 1) * p.blk;
-  int rq1 = r1;
-  if (r1 == nby && h_last != p.blk && h_last != p.blk / 2) rq1 = r1 - 1;
+  return r1 == nby && h_last != p.blk && h_last != p.blk / 2 ? r1 - 1 : r1;
+}
+
+// The persistent item kernel (and the generic kernel for what it leaves).
+static hipError_t launch_items(const SearchArgs& p, hipStream_t stream, int* used_fast) {
+  const int r0 = p.block_row_begin, r1 = p.block_row_end;
+  QsadGeom g;
+  int K = 0;
+  if (!cached_plan(p, &g, &K)) return launch_generic(p, 0, p.nbx, r0, r1 - r0, stream);
+  const int rq1 = qsad_rows_end(p, r1);
   hipError_t e = launch_fast(p, g, K, r0, rq1 - r0, stream);
   if (e != hipSuccess) return e;
   if (used_fast) *used_fast = 1;
@@ -1695,83 +1725,86 @@ static hipError_t launch_valu(const SearchArgs& p, hipStream_t stream, int* used
   return hipSuccess;
 }
 
-// Frame f of a batch as a single-frame search.
-static SearchArgs frame_args(const SearchArgs& p, int f) {
-  SearchArgs q = p;
-  q.nframes = 1;
-  q.ref = p.ref + (size_t)f * p.ref_fstride;
-  q.cur = p.cur + (size_t)f * p.cur_fstride;
-  q.ref_bytes = p.ref_bytes1;
-  q.cur_bytes = p.cur_bytes1;
-  q.ref_fstride = q.cur_fstride = 0;
-  q.mv = p.mv + 2 * (size_t)f * p.out_fstride;
-  if (p.cost) q.cost = p.cost + (size_t)f * p.out_fstride;
-  return q;
+// SAD jobs on the flow kernel where its plan (over every job's rows) takes
+// them, in launches of about one LDS ring of tiles per CU each: past the
+// ring, refills under compute starved the waves (8 1080p frames in one
+// launch: 22 % of wave time spinning on unpublished slots, 87 us per frame
+// against 69 for single frames; profiles/r03n_flow_stamps_batch.txt).
+// Returns false (nothing launched) when the flow kernel does not apply.
+static bool launch_flow_jobs(const SearchArgs& base, const SearchJob* jobs, int n, hipStream_t stream,
+                             hipError_t* err) {
+  *err = hipSuccess;
+  if (base.cost_kind != COST_SAD || n < 1) return false;
+  int rows = 0;
+  for (int i = 0; i < n; i++) {
+    rows += jobs[i].r1 - jobs[i].r0;
+    if ((uintptr_t)jobs[i].ref % 16 || (uintptr_t)jobs[i].cur % 16) return false;
+  }
+  SearchArgs probe = job_args(base, jobs[0]);
+  probe.block_row_begin = 0;
+  probe.block_row_end = rows;  // the planner counts tiles over every job's rows
+  QsadGeom g;
+  if (!cached_flow_plan(probe, &g)) return false;
+  long total = 0;
+  for (int i = 0; i < n; i++)
+    total += (long)g.wg_per_row * (qsad_rows_end(base, jobs[i].r1) - jobs[i].r0);
+  const long ring = (long)g.flow_slots * cu_count();
+  const long nl = (total + ring - 1) / ring;  // launches of about total / nl tiles
+  const long target = nl > 1 ? (total + nl - 1) / nl : total;
+  SearchJob fj[MAX_JOBS];
+  int m = 0;
+  long tiles = 0;
+  for (int i = 0; i < n && *err == hipSuccess; i++) {
+    SearchJob J = jobs[i];
+    J.r1 = qsad_rows_end(base, J.r1);
+    const long t = (long)g.wg_per_row * (J.r1 - J.r0);
+    if (m && (tiles + t > target || m == MAX_JOBS)) {
+      *err = launch_flow(base, g, fj, m, stream);
+      m = 0;
+      tiles = 0;
+    }
+    fj[m++] = J;
+    tiles += t;
+  }
+  if (m && *err == hipSuccess) *err = launch_flow(base, g, fj, m, stream);
+  // the rows and columns the flow kernel leaves, job by job
+  for (int i = 0; i < n && *err == hipSuccess; i++) {
+    const SearchArgs q = job_args(base, jobs[i]);
+    const int rq1 = qsad_rows_end(base, jobs[i].r1);
+    if (rq1 < jobs[i].r1) *err = launch_generic(q, 0, g.nbx_full, rq1, jobs[i].r1 - rq1, stream);
+    if (*err == hipSuccess && g.nbx_full < base.nbx)
+      *err = launch_generic(q, g.nbx_full, base.nbx - g.nbx_full, jobs[i].r0,
+                            jobs[i].r1 - jobs[i].r0, stream);
+  }
+  return true;
+}
+
+static hipError_t launch_valu(const SearchArgs& p, hipStream_t stream, int* used_fast) {
+  if (p.block_row_end <= p.block_row_begin) return hipSuccess;
+  const SearchJob J{p.ref, p.ref_row0, p.cur, p.cur_row0, p.block_row_begin, p.block_row_end, p.mv, p.cost};
+  hipError_t e;
+  if (launch_flow_jobs(p, &J, 1, stream, &e)) {
+    if (used_fast) *used_fast = 3;
+    return e;
+  }
+  return launch_items(p, stream, used_fast);
+}
+
+hipError_t launch_jobs(const SearchArgs& base, const SearchJob* jobs, int n, hipStream_t stream) {
+  hipError_t e;
+  if (n > 1 && launch_flow_jobs(base, jobs, n, stream, &e)) return e;
+  for (int i = 0; i < n; i++) {
+    if (jobs[i].r1 <= jobs[i].r0) continue;
+    e = launch_search(job_args(base, jobs[i]), stream, nullptr);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 hipError_t launch_search(const SearchArgs& p, hipStream_t stream, int* used_fast) {
   const int r0 = p.block_row_begin, r1 = p.block_row_end;
-  if (r1 <= r0 || p.nframes < 1) return hipSuccess;
+  if (r1 <= r0) return hipSuccess;
   if (used_fast) *used_fast = 0;
-  if (p.nframes > 1) {
-    // A batch: one flow-kernel launch over every frame's full-height rows
-    // (frame-major tiles) where the flow kernel takes the search; the rest
-    // (other costs and shapes, a frame's odd bottom row or partial right
-    // column) frame by frame.
-    QsadGeom g;
-    if (p.cost_kind == COST_SAD && cached_flow_plan(p, &g)) {
-      const int nby = (p.height + p.blk - 1) / p.blk;
-      const int h_last = p.height - (nby - 1) * p.blk;
-      int rq1 = r1;
-      if (r1 == nby && h_last != p.blk && h_last != p.blk / 2) rq1 = r1 - 1;
-      // At most one ring of tiles per CU per launch: every item is then staged
-      // at the start.  Past the ring, refills under compute starved the waves
-      // (a batch of 8 1080p frames: 22 % of wave time spinning on unpublished
-      // slots, 87 us per frame against 69 for single frames;
-      // profiles/r03n_flow_stamps_batch.txt), so bigger batches are cut into
-      // balanced sub-batches.
-      const long tiles_frame = (long)g.wg_per_row * (rq1 - r0);
-      const long ring = (long)g.flow_slots * cu_count();
-      if (tiles_frame * p.nframes > ring && p.nframes > 1) {
-        const int per_max = (int)(ring / tiles_frame > 1 ? ring / tiles_frame : 1);
-        const int nl = (p.nframes + per_max - 1) / per_max;
-        const int per = (p.nframes + nl - 1) / nl;
-        for (int f0 = 0; f0 < p.nframes; f0 += per) {
-          SearchArgs q = frame_args(p, f0);
-          q.nframes = min(per, p.nframes - f0);
-          q.ref_fstride = p.ref_fstride;
-          q.cur_fstride = p.cur_fstride;
-          q.ref_bytes = (uint32_t)((q.nframes - 1) * p.ref_fstride + p.ref_bytes1);
-          q.cur_bytes = (uint32_t)((q.nframes - 1) * p.cur_fstride + p.cur_bytes1);
-          const hipError_t e = launch_search(q, stream, used_fast);
-          if (e != hipSuccess) return e;
-        }
-        return hipSuccess;
-      }
-      SearchArgs q = p;
-      hipError_t e = hipSuccess;
-      if (rq1 > r0) {
-        q.block_row_end = rq1;  // the flow kernel's rows; records keep p's frame stride
-        e = launch_flow(q, g, r0, rq1 - r0, stream);
-        if (e != hipSuccess) return e;
-      }
-      if (used_fast) *used_fast = 3;
-      for (int f = 0; f < p.nframes; f++) {
-        const SearchArgs s = frame_args(p, f);
-        if (rq1 < r1 && (e = launch_generic(s, 0, g.nbx_full, rq1, r1 - rq1, stream)) != hipSuccess)
-          return e;
-        if (g.nbx_full < p.nbx &&
-            (e = launch_generic(s, g.nbx_full, p.nbx - g.nbx_full, r0, r1 - r0, stream)) != hipSuccess)
-          return e;
-      }
-      return hipSuccess;
-    }
-    for (int f = 0; f < p.nframes; f++) {
-      hipError_t e = launch_search(frame_args(p, f), stream, used_fast);
-      if (e != hipSuccess) return e;
-    }
-    return hipSuccess;
-  }
   if (p.cost_kind == COST_SSIM) return launch_ssim(p, stream);
   MfmaGeom mg;
   if (p.cost_kind == COST_SSD && p.scratch && plan_mfma_ssd(p, &mg) &&

@@ -185,6 +185,33 @@ class Engine:
             cost_t.data_ptr() if cost_t is not None else None, st), self._h)
 
 
+    def search_stripes_device(self, width: int, height: int, blk: int, span: int, cost, jobs,
+                              stream=None, stride=None):
+        """Several stripes in one call (me_search_stripes_device).  jobs: list of
+        (ref_t, ref_row0, cur_t, cur_row0, row_begin, row_end, mv_t, cost_t) --
+        the arguments of one search_stripe_device each (tensors (rows, pitch))."""
+        self.prepared_stripes_search(width, height, blk, span, cost, jobs, stream, stride)()
+
+    def prepared_stripes_search(self, width, height, blk, span, cost, jobs, stream=None,
+                                stride=None):
+        """Zero-argument callable enqueueing search_stripes_device(...) with these buffers."""
+        arr = (StripeJob * len(jobs))()
+        for a, (rt, r0, ct, c0, b0, b1, mv, co) in zip(arr, jobs):
+            a.d_ref, a.ref_row0, a.d_cur, a.cur_row0 = rt.data_ptr(), r0, ct.data_ptr(), c0
+            a.block_row_begin, a.block_row_end = b0, b1
+            a.d_mv_xy, a.d_block_cost = mv.data_ptr(), co.data_ptr() if co is not None else None
+        pitch = stride or jobs[0][0].stride(0) * jobs[0][0].element_size()
+        fn, h = _lib.lib().me_search_stripes_device, self._h
+        args = (h, width, height, pitch, blk, span, cost_code(cost), arr, len(jobs),
+                stream if stream is not None else _current_stream())
+
+        def run():
+            s = fn(*args)
+            if s:
+                check(s, h)
+        run.jobs = arr  # keep the descriptor array alive with the callable
+        return run
+
     def search_batch_device(self, ref_t, ref_row0: int, cur_t, cur_row0: int, width: int,
                             height: int, blk: int, span: int, cost, row_begin: int, row_end: int,
                             mv_t, cost_t=None, stream=None, stride=None):
@@ -302,6 +329,14 @@ class Engine:
             if s:
                 check(s, h)
         return run
+
+
+class StripeJob(ctypes.Structure):
+    """include/me.h me_stripe_job."""
+    _fields_ = [("d_ref", ctypes.c_void_p), ("ref_row0", ctypes.c_int),
+                ("d_cur", ctypes.c_void_p), ("cur_row0", ctypes.c_int),
+                ("block_row_begin", ctypes.c_int), ("block_row_end", ctypes.c_int),
+                ("d_mv_xy", ctypes.c_void_p), ("d_block_cost", ctypes.c_void_p)]
 
 
 class Graph:

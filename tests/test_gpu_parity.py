@@ -436,3 +436,44 @@ def test_batch_search_argument_checks(engine):
     assert call(n=0) == me._lib.ME_EINVAL
     assert call(ref_stride=1 << 31) == me._lib.ME_EUNSUPPORTED
     torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("cost,blk,span,w,h,ways", [
+    ("sad", 16, 32, 1920, 1080, 8),   # flow kernel: one launch for stripes of different rows
+    ("sad", 16, 32, 1920, 1080, 4),
+    ("sad", 16, 16, 1000, 700, 3),    # per-job item / generic kernels
+    ("ssd", 16, 32, 1920, 1080, 8),   # matrix cores, job by job
+])
+def test_stripe_jobs_of_different_rows(engine, cost, blk, span, w, h, ways):
+    """me_search_stripes_device with bench.py's rotated step: job f is stripe
+    (r + f) % N of frame f, so one call mixes top, interior and bottom stripes
+    of different heights; every job equals the oracle on its rows."""
+    import torch
+    from motionestimation_amd import shard
+    F = max(ways, 3)
+    base_ref, base_cur = synth.frame_pair(w, h, 41, -5, 2)
+    frames = [(np.roll(base_ref, 37 * f, axis=1), np.roll(base_cur, 37 * f, axis=1))
+              for f in range(F)]
+    plan = shard.plan(w, h, blk, span, ways)
+    for r in (0, ways - 1):
+        jobs, want = [], []
+        for f in range(F):
+            st = plan[(r + f) % ways]
+            if not st.nblocks:
+                continue
+            rt = torch.from_numpy(frames[f][0][st.ref_y0:st.ref_y1].copy()).cuda()
+            ct = torch.from_numpy(frames[f][1][st.cur_y0:st.cur_y1].copy()).cuda()
+            mv = torch.full((st.nblocks, 2), -3, dtype=torch.int16, device="cuda")
+            co = torch.zeros(st.nblocks, dtype=torch.int32, device="cuda")
+            jobs.append((rt, st.ref_y0, ct, st.cur_y0, st.row_begin, st.row_end, mv, co))
+            want.append((f, st))
+        for _ in range(2):
+            engine.search_stripes_device(w, h, blk, span, cost, jobs)
+        torch.cuda.synchronize()
+        for (f, st), job in zip(want, jobs):
+            omv, oco, _ = O.full_search(*frames[f], blk, span, cost, threads=NT,
+                                        begin=st.row_begin * st.nbx, end=st.row_end * st.nbx)
+            msg = f"{cost} {w}x{h} rank {r} frame {f} rows {st.row_begin}:{st.row_end}"
+            np.testing.assert_array_equal(job[6].cpu().numpy(), omv, err_msg=msg)
+            np.testing.assert_array_equal(job[7].cpu().numpy().view(np.uint32), oco, err_msg=msg)
+    engine.device_check()

@@ -5,7 +5,8 @@ BASELINE config and time every rank's stripe search (its halo-only planes,
 me_full_search_stripe_device) back to back on this GPU.  The slowest stripe is
 the compute-bound step time of the N-GPU strong-scaling run (before the
 RCCL gather), so t(N=1) / max_r t_r(N) is the compute-side speed-up ceiling.
---frames F times F frames' stripes per launch (the batched step of bench.py).
+--frames F times a rank's F-frame step as bench.py runs it: stripe (r + f) % N
+of frame f for rank r, all in one me_search_stripes_device call.
 One JSON line per N (times per launch, i.e. per F frames).
 
   python tools/stripe_sweep.py [--config 1080p|4k|8k] [--cost sad] [--ranks 1,2,4,8]
@@ -52,23 +53,28 @@ def main():
             eng.full_search_device(rt0, ct0, blk, span, a.cost, mv0, co0)
         torch.cuda.synchronize()
     base = None
+    F = a.frames
+    frames = [(np.roll(ref, 37 * f, axis=1), np.roll(cur, 37 * f, axis=1)) for f in range(F)]
     for n in [int(x) for x in a.ranks.split(",")]:
         times = []
-        for st in shard.plan(w, h, blk, span, n):
-            if not st.nblocks:
+        plan = shard.plan(w, h, blk, span, n)
+        for r in range(n):
+            # rank r's step: stripe (r + f) % n of frame f (bench.py StripeRun)
+            own = [plan[(r + f) % n] for f in range(F)]
+            jobs, keep = [], []
+            for f, st in enumerate(own):
+                if not st.nblocks:
+                    continue
+                rt = torch.from_numpy(frames[f][0][st.ref_y0:st.ref_y1].copy()).cuda()
+                ct = torch.from_numpy(frames[f][1][st.cur_y0:st.cur_y1].copy()).cuda()
+                mv = torch.empty((st.nblocks, 2), dtype=torch.int16, device="cuda")
+                co = torch.empty(st.nblocks, dtype=torch.int32, device="cuda")
+                keep += [rt, ct, mv, co]
+                jobs.append((rt, st.ref_y0, ct, st.cur_y0, st.row_begin, st.row_end, mv, co))
+            if not jobs:
                 times.append(0.0)
                 continue
-            F = a.frames
-            rt = torch.from_numpy(np.stack([np.roll(ref, 37 * f, axis=1)[st.ref_y0:st.ref_y1]
-                                            for f in range(F)])).cuda()
-            ct = torch.from_numpy(np.stack([np.roll(cur, 37 * f, axis=1)[st.cur_y0:st.cur_y1]
-                                            for f in range(F)])).cuda()
-            mv = torch.empty((F * st.nblocks, 2), dtype=torch.int16, device="cuda")
-            co = torch.empty(F * st.nblocks, dtype=torch.int32, device="cuda")
-
-            def run():
-                eng.search_batch_device(rt, st.ref_y0, ct, st.cur_y0, w, h, blk, span, a.cost,
-                                        st.row_begin, st.row_end, mv, co)
+            run = eng.prepared_stripes_search(w, h, blk, span, a.cost, jobs, stride=w)
             for _ in range(5):
                 run()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
