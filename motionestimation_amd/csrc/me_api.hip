@@ -64,6 +64,7 @@ static Tuning read_tuning() {
   env_int("ME_FLOW", 0, 1, &t.flow);
   env_int("ME_FLOW_SLOTS", 2, 16, &t.flow_slots);
   env_int("ME_PRIO", 0, 1, &t.prio);
+  env_int("ME_STRIP", 0, 64, &t.strip);
   return t;
 }
 const Tuning& tuning() {

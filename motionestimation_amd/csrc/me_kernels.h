@@ -57,6 +57,9 @@ struct QsadGeom {
   int threads;     // workgroup size
   int lds;         // dynamic LDS bytes
   int wg_per_row;  // workgroups per block row
+  int strip_w;     // > 0: tiles run in vertical strips of strip_w tile columns, each
+                   // strip top to bottom (wide frames: an XCD's L2 keeps the strip's
+                   // window rows while the tile rows that read them pass)
   int nbx_full;    // full-width blocks per row
   int aligned;     // 4-byte aligned global rows
   int tile16;      // ref tile staged in 16-byte granules (X0, width, rows 16-byte aligned)

@@ -486,8 +486,19 @@ __device__ __forceinline__ Item item_of(const SearchArgs& p, const QsadGeom& g, 
                                         int pass) {
   Item it;
   it.j = 0;
-  it.bx0 = (tile % g.wg_per_row) * g.tb;
-  it.by = g.row0 + tile / g.wg_per_row;
+  if (g.strip_w > 0) {
+    // strip-major: strip s holds tile columns [s * sw, s * sw + its width),
+    // walked row by row (the last strip may be narrower)
+    const int sw = g.strip_w, per = sw * g.nrows;
+    const int s = tile / per, r = tile - s * per;
+    const int w = min(sw, g.wg_per_row - s * sw);
+    const int row = r / w;
+    it.bx0 = (s * sw + (r - row * w)) * g.tb;
+    it.by = g.row0 + row;
+  } else {
+    it.bx0 = (tile % g.wg_per_row) * g.tb;
+    it.by = g.row0 + tile / g.wg_per_row;
+  }
   it.nb = min(g.tb, g.nbx_full - it.bx0);
   it.tly = it.by * B;
   it.h = min(B, p.height - it.tly);
@@ -1345,6 +1356,12 @@ bool plan_fast(const SearchArgs& p, QsadGeom* g, int* k_out) {
   }
   g->prio = tu.prio != 0;
   g->flow_slots = 0;
+  // Wide frames: vertical strips of 16 tiles (8K 8x8: 1,024 pixels plus the
+  // window's 2S), so an XCD's contiguous run of the order is a few whole
+  // strips and its L2 holds a strip's window rows while they are reread
+  // (the row-major order fetched 2.4x the algorithmic bytes at 8K SAD).
+  g->strip_w = g->wg_per_row >= 32 && rows >= 32 ? 16 : 0;
+  if (tu.strip >= 0) g->strip_w = tu.strip;
   *k_out = bK;
   return true;
 }
@@ -1454,6 +1471,7 @@ bool plan_flow(const SearchArgs& p, QsadGeom* g) {
   if (tuning().flow_slots && tuning().flow_slots < best_ns) best_ns = tuning().flow_slots;
   q.flow_slots = best_ns;
   q.prio = tuning().prio != 0;
+  q.strip_w = 0;
   q.lds = best_ns * slot + best_ns * q.tb * 8 + (int)sizeof(int) * 40;
   return q.lds <= 160 * 1024;
 }

@@ -23,6 +23,7 @@ struct Tuning {
   int flow = -1;          // ME_FLOW=0|1: SAD flow kernel off / allowed (-1 = automatic)
   int flow_slots = 0;     // ME_FLOW_SLOTS=2..16: flow kernel LDS ring slots (0 = automatic)
   int prio = -1;          // ME_PRIO=0|1: staging waves raise their issue priority (-1 = automatic: on)
+  int strip = -1;         // ME_STRIP=0..64: item-kernel tile strips (0 = row-major; -1 = automatic)
 };
 
 const Tuning& tuning();
