@@ -186,7 +186,7 @@ def cpu_baselines(ref, cur, blk, span, cost, threads, cands):
     return out
 
 
-def host_stream(eng, w, h, blk, span, cost, seed, sx, sy, kern_ms, cands_frame):
+def host_stream(eng, w, h, blk, span, cost, seed, sx, sy, frame_ms, cands_frame):
     """Frame-pair streaming from host memory (me_search_pairs):
     a synthetic pan, consecutive pairs, frames uploaded over PCIe inside the
     timed call (pinned: direct DMA; pageable: staged), MV records copied back.
@@ -208,7 +208,7 @@ def host_stream(eng, w, h, blk, span, cost, seed, sx, sy, kern_ms, cands_frame):
         dt = (time.perf_counter() - t0) / reps
         out[name] = {"pairs_per_s": npairs / dt, "candidates_per_s": cands_frame * npairs / dt,
                      "ms_per_pair": dt / npairs * 1e3}
-    out["kernel_only_pairs_per_s"] = 1e3 / kern_ms
+    out["kernel_only_pairs_per_s"] = 1e3 / frame_ms  # one frame's kernel time, inputs in HBM
     del pinned
     return out
 
@@ -650,14 +650,22 @@ def main():
     # VALU work: the exact abs-diff count (w*h of each block, not B*B).
     # Stripe mode: the frame's work / N against the slowest rank's kernel time.
     # A launch searches the step's F frames (F stripes in stripe mode).
+    # Frames mode: the step's F frames go out as launches of one frame each
+    # (launch_flow_jobs groups about one LDS ring of tiles per launch, and every
+    # BASELINE frame is more than half a ring; SSD and the item kernel launch per
+    # job), so a launch is one frame: its bytes over kern_ms / F.  Stripe mode:
+    # the rank's F stripes (one ring of tiles per launch at N = 8, a few
+    # launches at N = 2, 4) are priced as a whole step.
     if mode == "frames":
-        alg_bytes = F * (2 * w * h + 8 * nb)
+        alg_bytes = 2 * w * h + 8 * nb
+        launch_ms = kern_ms / F
         absdiffs = F * exact_absdiffs(w, h, blk, span)
     else:
         alg_bytes = sum((o.ref_y1 - o.ref_y0 + o.cur_y1 - o.cur_y0) * w + 8 * o.nblocks
                         for o in sr.own)
+        launch_ms = kern_ms
         absdiffs = F * exact_absdiffs(w, h, blk, span) / world
-    achieved = alg_bytes / (kern_ms / 1e3) / 1e9
+    achieved = alg_bytes / (launch_ms / 1e3) / 1e9
     tag = f"{args.config}_b{blk}_s{span}_{args.cost}"
     traffic, traffic_search = load_traffic(tag)
     line = {
@@ -687,6 +695,7 @@ def main():
                    "candidates_per_frame": cands_frame, "blocks_per_frame": nb,
                    "frames_per_step": F, "parallelism": f"{mode}{world}"},
         "kernel_ms": kern_ms,
+        "launch_ms": launch_ms,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_per_search": traffic_search,
@@ -737,7 +746,7 @@ def main():
             line["stripe_4k"] = rec4k
     if rank == 0 and world == 1 and mode == "frames" and not args.no_stream:
         line["host_stream"] = host_stream(eng, w, h, blk, span, args.cost, seed, sx, sy,
-                                          kern_ms, cands_frame)
+                                          launch_ms, cands_frame)
     if rank == 0:
         print(json.dumps(line), file=json_out, flush=True)
     eng.close()

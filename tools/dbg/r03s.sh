@@ -1,0 +1,5 @@
+set -e
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/r03s_pytest_gpu.log 2>&1
+bash tools/profile_all.sh r03s
