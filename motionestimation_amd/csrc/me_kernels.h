@@ -110,7 +110,7 @@ struct MfmaGeom {
   int row0, nrows, nbx;
   int tiles_x, tiles_y;
   int ngx;               // 64-position groups per tile
-  int ngxw;              // groups per workgroup (1 or 2; 4 waves each)
+  int ngxw;              // groups per workgroup (16x16 tiles: 1 or 2, 4 waves each; 8x8: all, in turn)
   int km;                // candidate rows per chunk L = 13 + 16 km
   int bm, bm_wpr, bm_lp; // block-major kernel (16x16, S <= 103); workgroups per block row; window pitch
   int lds;               // dynamic LDS bytes

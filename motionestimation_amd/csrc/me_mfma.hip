@@ -633,8 +633,10 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd16_kernel(SearchArgs p, 
 //   key = ((S2 + 1) << 6) + (y - y0) + (acc << 7) = (SSD - p + 1) << 6 | (y - y0)
 // SSD <= 64 * 255^2 < 2^22, so valid keys < 2^28; x out of window: acc + 2^22
 // (keys in [2^29, 2^30)); y out of window: bit 31.  Chunks of L = 16 KM8 rows (48).
-// Workgroup = (tile, one group of 64 candidate columns), 4 waves (phase s);
-// tiles spanning several workgroups merge like the 16x16 kernel.
+// Workgroup = one tile, 4 waves (phase s), walking the tile's groups of 64
+// candidate columns one after another: the (cost, dy, dx) keys meet in LDS and
+// leave once, with no cross-workgroup merge (per-group workgroups merged through
+// device-scope atomics that reach memory: 35 MB of the 8K search's writes).
 template <int KM8>
 __global__ __launch_bounds__(256)
 __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd8_kernel(SearchArgs p, MfmaGeom g) {
@@ -652,8 +654,7 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd8_kernel(SearchArgs p, M
   const int tid = (int)threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n = lane & 15, h = lane >> 4;
   const int S = p.range, W = p.width, H = p.height;
-  const int wpt = g.ngx;  // one group per workgroup
-  int tile, gx;
+  int tile;
   {
     // Workgroups in vertical strips of SSD8_STRIP tile columns, each strip
     // walked down its tile rows (then across the strip, then the groups); each
@@ -665,12 +666,10 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd8_kernel(SearchArgs p, M
     const int x = bid & 7, m = bid >> 3, q = nwg >> 3, rem = nwg & 7;
     const int lin = x * q + min(x, rem) + m;
     const int sw = min(SSD8_STRIP, g.tiles_x);
-    const int per_strip = g.tiles_y * sw * wpt;
+    const int per_strip = g.tiles_y * sw;
     const int st = lin / per_strip, r = lin - st * per_strip;
     const int sws = min(sw, g.tiles_x - st * sw);  // the last strip may be narrower
-    const int ty = r / (sws * wpt), r2 = r - ty * (sws * wpt);
-    const int txl = r2 / wpt;
-    gx = r2 - txl * wpt;
+    const int ty = r / sws, txl = r - ty * sws;
     tile = ty * g.tiles_x + st * sw + txl;
   }
   const int tx = tile % g.tiles_x, ty = tile / g.tiles_x;
@@ -679,10 +678,10 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd8_kernel(SearchArgs p, M
   const int tlx0 = 8 * bc0, tly0 = 8 * br0;
   const int xa = max(tlx0 - S, 0), xb = min(tlx0 + 8 * (nbc - 1) + S, W - 8);
   const int ya = max(tly0 - S, 0), yb = min(tly0 + 8 * (nbr - 1) + S, H - 8);
-  const int ngx = (xb - xa + 1 + 63) >> 6;
-  if (gx >= ngx) return;  // uniform; the tile's arrival count is ngx
+  const int ngx = (xb - xa + 1 + 63) >> 6;  // groups of 64 positions this tile needs
   const int nch = (yb - ya + 1 + L - 1) / L;
-  const int X0 = (xa + 64 * gx) & ~3;
+  int gx = 0;                 // the group being searched
+  int X0 = xa & ~3;           // its window column origin
 
   const __amdgpu_buffer_rsrc_t rrp =
       __builtin_amdgcn_make_buffer_rsrc((void*)g.rp, (short)0, g.rp_bytes, 0x00020000);
@@ -756,7 +755,6 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd8_kernel(SearchArgs p, M
 
   uint32_t sumLH, Cv;
   const int s = wave;
-  const int xn = xa + 64 * gx + 4 * n + s;
   {
     const int tly = tly0 + 8 * h;
     int lo = max(tly - S, 0), hi = min(tly + S, H - 8);
@@ -764,7 +762,17 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd8_kernel(SearchArgs p, M
     sumLH = (uint32_t)(lo + hi);
     Cv = 0x80000000u - (uint32_t)(hi - lo) - 1u;
   }
-  const int u = xn - X0, sig = u & 3, ccol = u - sig;
+  // x_n - X0 = (xa & 3) + 4n + s whatever the group: fixed LDS lane offsets
+  const int u = (xa & 3) + 4 * n + s, sig = u & 3, ccol = u - sig;
+  const uint32_t lbase = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) uint8_t*)smem);
+  const uint32_t lds_lane = lbase + (uint32_t)(sig * COPY + 2 * h * WP + ccol);
+  const uint32_t s2t_lane = (uint32_t)(uintptr_t)(
+      (__attribute__((address_space(3))) uint8_t*)s2t) + (uint32_t)(4 * n + s) * 4u;
+  typedef __attribute__((address_space(3))) const int lds_i32;
+
+  for (; gx < ngx; gx++) {
+  X0 = (xa + 64 * gx) & ~3;
+  const int xn = xa + 64 * gx + 4 * n + s;
   v4i initv;
 #pragma unroll
   for (int r = 0; r < 4; r++) {
@@ -774,15 +782,9 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd8_kernel(SearchArgs p, M
     const int c = cc[4 * h + r];
     initv[r] = ok ? (c >> 1) : (c >> 1) + (1 << 22);
   }
-  const uint32_t lbase = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) uint8_t*)smem);
-  const uint32_t lds_lane = lbase + (uint32_t)(sig * COPY + 2 * h * WP + ccol);
-  const uint32_t s2t_lane = (uint32_t)(uintptr_t)(
-      (__attribute__((address_space(3))) uint8_t*)s2t) + (uint32_t)(4 * n + s) * 4u;
-  typedef __attribute__((address_space(3))) const int lds_i32;
-
   for (int ch = 0; ch < nch; ch++) {
     const int y0 = ya + ch * L;
-    if (ch > 0) {
+    if (ch > 0 || gx > 0) {
       __syncthreads();
       stage(y0);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -867,38 +869,16 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd8_kernel(SearchArgs p, M
       }
     }
   }
+  }  // groups
   __syncthreads();
   const int br = tid >> 2, bc = tid & 3;
-  const bool outb = tid < 16 && br < nbr && bc < nbc;
-  unsigned long long* gk = g.mkeys + 16 * (size_t)tile + tid;
-  bool last = ngx == 1;
-  if (!last) {
-    int* flag = reinterpret_cast<int*>(keys + 16);
-    if (outb) {
-      const unsigned long long old = __hip_atomic_fetch_min(gk, keys[tid], __ATOMIC_RELAXED,
-                                                            __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("s_waitcnt vmcnt(0)" : : "v"((uint32_t)old) : "memory");
-    }
-    __syncthreads();
-    if (tid == 0) {
-      const unsigned arrived = __hip_atomic_fetch_add(g.mcnt + tile, 1u, __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_AGENT);
-      flag[0] = arrived == (unsigned)ngx - 1u;
-    }
-    __syncthreads();
-    last = flag[0] != 0;
-  }
-  if (last && outb) {
-    const unsigned long long kk =
-        ngx == 1 ? keys[tid]
-                 : __hip_atomic_exchange(gk, ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid < 16 && br < nbr && bc < nbc) {
+    const unsigned long long kk = keys[tid];
     const int out = (br0 + br - p.block_row_begin) * p.nbx + bc0 + bc;
     p.mv[2 * out] = (int16_t)((int)(kk & 0xFFFF) - 32768);
     p.mv[2 * out + 1] = (int16_t)((int)((kk >> 16) & 0xFFFF) - 32768);
     if (p.cost) p.cost[out] = (uint32_t)(kk >> 32);
   }
-  if (last && ngx > 1 && tid == 0)
-    __hip_atomic_store(g.mcnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ------------------------------------------------- 16x16, block-major tiles
@@ -1246,7 +1226,7 @@ bool mfma_disabled() { return kernel_path() == 1; }
 
 // Tiles of a B = 16 search over block rows [begin, end) (the merge buffers' size).
 size_t mfma_merge_tiles(const SearchArgs& p) {
-  if ((p.blk != 16 && p.blk != 8) || p.width < p.blk) return 0;
+  if (p.blk != 16 || p.width < p.blk) return 0;  // 8x8: no cross-workgroup merge
   const size_t tx = (size_t)((p.width / p.blk + 3) / 4);
   const size_t ty = (size_t)((p.block_row_end - p.block_row_begin + 3) / 4);
   return tx * ty;
@@ -1350,7 +1330,8 @@ bool plan_mfma_ssd(const SearchArgs& p, MfmaGeom* g) {
 }
 
 // 8x8 blocks: full-height block rows only (a partial bottom row goes to the
-// VALU kernels), one 64-column group per workgroup, chunks of 16 ME_SSD8_KM rows.
+// VALU kernels), one workgroup per 4x4-block tile walking its 64-column groups,
+// chunks of 16 ME_SSD8_KM rows.
 static bool plan_mfma_ssd8(const SearchArgs& p, MfmaGeom* g) {
   if (mfma_disabled()) return false;
   const int S = p.range, W = p.width, H = p.height;
@@ -1371,8 +1352,7 @@ static bool plan_mfma_ssd8(const SearchArgs& p, MfmaGeom* g) {
   g->tiles_y = (g->nrows + 3) / 4;
   const int nxmax = min(24 + 2 * S + 1, W - 7);
   g->ngx = (nxmax + 63) / 64;
-  g->ngxw = 1;
-  if (g->ngx > 1 && (!p.mkeys || !p.mcnt || p.merge_tiles < mfma_merge_tiles(p))) return false;
+  g->ngxw = g->ngx;  // one workgroup walks all of a tile's groups
   g->km = ME_SSD8_KM;  // L = 16 km candidate rows per chunk
   const int L = 16 * g->km;
   g->lds = 4 * (L + 8) * ME_SSD8_WP + 16 * 8 + 16 * 4 + (L + 1) * 256;
@@ -1409,7 +1389,7 @@ hipError_t launch_mfma_ssd(const SearchArgs& p, const MfmaGeom& g, hipStream_t s
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   if (p.blk == 8) {
-    const dim3 grid8((unsigned)(g.tiles_x * g.tiles_y * g.ngx));
+    const dim3 grid8((unsigned)(g.tiles_x * g.tiles_y));
     e = lds_attr((const void*)me_mfma_ssd8_kernel<ME_SSD8_KM>, g.lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(me_mfma_ssd8_kernel<ME_SSD8_KM>, grid8, dim3(256), g.lds, stream, p, g);
