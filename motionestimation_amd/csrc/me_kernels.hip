@@ -511,20 +511,40 @@ __device__ __forceinline__ Item item_of(const SearchArgs& p, const QsadGeom& g, 
   return it;
 }
 
-// Issue the staging of one item into an LDS buffer: asynchronous LDS DMA on
-// the aligned path (no VGPR round trip, completes under the previous item's
-// compute), synchronous byte copies otherwise.
+// Tile of a launch over a job table -> (job, tile of that job's rows): jobs
+// are consecutive tile ranges (jb.tile_pre), every job the same frame
+// geometry; a job's planes and records are its own.
+template <int B, int K>
+__device__ __forceinline__ Item job_item(const SearchArgs& p, const QsadGeom& g,
+                                         const FlowJobs& jb, int tile, int pass) {
+  int j = 0;
+  while (j + 1 < jb.n && jb.tile_pre[j + 1] <= tile) j++;
+  QsadGeom gj = g;
+  gj.row0 = jb.r0[j];
+  if (g.strip_w > 0) gj.nrows = (jb.tile_pre[j + 1] - jb.tile_pre[j]) / g.wg_per_row;  // strip walk
+  Item it = item_of<B, K>(p, gj, tile - jb.tile_pre[j], pass);
+  it.j = j;
+  return it;
+}
+
+// Issue the staging of one item into an LDS buffer from its job's planes:
+// asynchronous LDS DMA on the aligned path (no VGPR round trip, completes
+// under the previous item's compute), synchronous byte copies otherwise.
 template <int B>
 __device__ __forceinline__ void stage_item(const SearchArgs& p, const QsadGeom& g, const Item& it,
-                                           uint8_t* buf, __amdgpu_buffer_rsrc_t rref,
-                                           __amdgpu_buffer_rsrc_t rcur) {
+                                           uint8_t* buf, const FlowJobs& jb) {
   uint8_t* tile = buf;
   uint8_t* cur = buf + g.tile_bytes;
   const int pitch = g.pitch, stride = p.stride;
   const int tid = fresh_tid(), nthr = blockDim.x;
+  const int ref_row0 = jb.ref_row0[it.j], cur_row0 = jb.cur_row0[it.j];
   if (g.aligned) {
+    const __amdgpu_buffer_rsrc_t rref = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)jb.ref[it.j], (short)0, jb.ref_bytes[it.j], 0x00020000);
+    const __amdgpu_buffer_rsrc_t rcur = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)jb.cur[it.j], (short)0, jb.cur_bytes[it.j], 0x00020000);
     // tile byte (r, x) <- ref(prow0 + r, X0 + x); zeros outside the resident rows.
-    const int base = (it.prow0 - p.ref_row0) * stride + it.X0;
+    const int base = (it.prow0 - ref_row0) * stride + it.X0;
     auto src = [&](int d) {
       const int r = (int)__umulhi((uint32_t)d, g.pitch_magic), x = d - r * pitch;
       return (uint32_t)(base + r * stride + x);
@@ -536,7 +556,7 @@ __device__ __forceinline__ void stage_item(const SearchArgs& p, const QsadGeom& 
     else
       dma4(rref, tile, it.prows * pitch, src);
     // cur block b, row oy -> LDS bytes (b * B + oy) * B
-    const int cbase = (it.tly - p.cur_row0) * stride + it.bx0 * B;
+    const int cbase = (it.tly - cur_row0) * stride + it.bx0 * B;
     if constexpr (B == 16) {
       dma16(rcur, cur, it.nb * B * B, [&](int d) {
         return (uint32_t)(cbase + ((d >> 4) & 15) * stride + (d >> 8) * B);
@@ -551,32 +571,30 @@ __device__ __forceinline__ void stage_item(const SearchArgs& p, const QsadGeom& 
       const int r = i / pitch, x = i - r * pitch;
       const int y = it.prow0 + r, xx = it.X0 + x;
       tile[i] = (y >= 0 && y < p.height && xx >= 0 && xx < p.width)
-                    ? row_ptr(p, p.ref, p.ref_row0, y)[xx] : 0;
+                    ? row_ptr(p, jb.ref[it.j], ref_row0, y)[xx] : 0;
     }
     for (int i = tid; i < it.nb * B * B; i += nthr) {
       const int b = i / (B * B), rem = i - b * B * B, oy = rem / B, x = rem - oy * B;
-      cur[i] = oy < it.h ? row_ptr(p, p.cur, p.cur_row0, it.tly + oy)[(it.bx0 + b) * B + x] : 0;
+      cur[i] = oy < it.h ? row_ptr(p, jb.cur[it.j], cur_row0, it.tly + oy)[(it.bx0 + b) * B + x] : 0;
     }
   }
 }
 
-// Persistent, double-buffered search.  The grid is sized to what fits on the
-// chip at once; workgroups sharing an XCD (bid % 8, a speed heuristic only)
-// walk one contiguous band of tiles, so each XCD's L2 holds one band of rows.
-// Item k of a workgroup = (its k / passes-th tile, pass k % passes); while
-// item k is computed from LDS buffer k & 1, item k + 1 streams into the other.
+// Persistent, double-buffered search over a job table (one frame, or the
+// frames / stripes of a batch: every job's tiles, job-major).  The grid is
+// sized to what fits on the chip at once; workgroups sharing an XCD (bid % 8,
+// a speed heuristic only) walk one contiguous band of tiles, so each XCD's L2
+// holds one band of rows.  Item k of a workgroup = (its k / passes-th tile,
+// pass k % passes); while item k is computed from LDS buffer k & 1, item k + 1
+// streams into the other.
 template <int COST, int B, int K, int PC = 0>
-__global__ __launch_bounds__(1024) void me_fast_kernel(SearchArgs p, QsadGeom g) {
+__global__ __launch_bounds__(1024) void me_fast_kernel(SearchArgs p, QsadGeom g, FlowJobs jb) {
   constexpr int CW = B / 4;
   extern __shared__ __align__(16) uint8_t smem[];
   const int buf_bytes = g.tile_bytes + g.tb * B * B;
   uint64_t* keys = reinterpret_cast<uint64_t*>(smem + 2 * buf_bytes);
   const int tid = threadIdx.x, nthr = blockDim.x;
   const int S = p.range;
-  const __amdgpu_buffer_rsrc_t rref =
-      __builtin_amdgcn_make_buffer_rsrc((void*)p.ref, (short)0, p.ref_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rcur =
-      __builtin_amdgcn_make_buffer_rsrc((void*)p.cur, (short)0, p.cur_bytes, 0x00020000);
 
   // Tiles of this workgroup come from the band of its XCD group x (bid % 8,
   // a speed heuristic only).  Dynamic (p.sched != null): the group's
@@ -584,7 +602,7 @@ __global__ __launch_bounds__(1024) void me_fast_kernel(SearchArgs p, QsadGeom g)
   // take more; tile ids are pulled two tiles ahead into an LDS ring so the
   // double-buffered staging always knows its next item.  Static otherwise:
   // member m of n_x takes band tiles m, m + n_x, ...
-  const int ntiles = g.wg_per_row * g.nrows;
+  const int ntiles = jb.tile_pre[jb.n];
   const int nwg = (int)gridDim.x, bid = (int)blockIdx.x;
   const int ng = nwg < 8 ? nwg : 8;  // XCD groups that have workgroups
   const int x = bid % ng, m = bid / ng;
@@ -647,10 +665,10 @@ __global__ __launch_bounds__(1024) void me_fast_kernel(SearchArgs p, QsadGeom g)
   int nitems = 0;
 #endif
   int tile = tile_at(0);
-  if (tile >= 0) stage_item<B>(p, g, item_of<B, K>(p, g, tile, 0), smem, rref, rcur);
+  if (tile >= 0) stage_item<B>(p, g, job_item<B, K>(p, g, jb, tile, 0), smem, jb);
   const int G = g.groups;
   for (int k = 0; tile >= 0; k++) {
-    const Item it = item_of<B, K>(p, g, tile, pass);
+    const Item it = job_item<B, K>(p, g, jb, tile, pass);
     uint8_t* buf = smem + (k & 1) * buf_bytes;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();  // item k staged by every wave; item k-1 fully consumed
@@ -665,8 +683,8 @@ __global__ __launch_bounds__(1024) void me_fast_kernel(SearchArgs p, QsadGeom g)
       const int npass = pass + 1 < passes ? pass + 1 : 0;
       if (g.prio) __builtin_amdgcn_s_setprio(3);
       if (ntile >= 0)
-        stage_item<B>(p, g, item_of<B, K>(p, g, ntile, npass), smem + ((k + 1) & 1) * buf_bytes,
-                      rref, rcur);
+        stage_item<B>(p, g, job_item<B, K>(p, g, jb, ntile, npass),
+                      smem + ((k + 1) & 1) * buf_bytes, jb);
       if (g.prio) __builtin_amdgcn_s_setprio(0);
     }
 #ifdef ME_STAMPS
@@ -782,9 +800,10 @@ __global__ __launch_bounds__(1024) void me_fast_kernel(SearchArgs p, QsadGeom g)
         uint64_t none = ~0ull;  // materialised here, not kept live (it spilled)
         asm volatile("" : "+v"(none));
         keys[tid] = none;  // ready for this workgroup's next tile
-        const int out = (it.by - p.block_row_begin) * p.nbx + it.bx0 + tid;
-        p.mv[2 * out] = (int16_t)((int)(kk & 0xFFFF) - 32768);
-        p.mv[2 * out + 1] = (int16_t)((int)((kk >> 16) & 0xFFFF) - 32768);
+        const int out = (it.by - jb.r0[it.j]) * p.nbx + it.bx0 + tid;
+        int16_t* mv = jb.mv[it.j];
+        mv[2 * out] = (int16_t)((int)(kk & 0xFFFF) - 32768);
+        mv[2 * out + 1] = (int16_t)((int)((kk >> 16) & 0xFFFF) - 32768);
         uint32_t cost = (uint32_t)(kk >> 32);
         if constexpr (COST == COST_SSD) {  // biased v -> SSD: + sum c^2 of the block
           const uint32_t* cb = reinterpret_cast<const uint32_t*>(buf + g.tile_bytes) + tid * B * CW;
@@ -793,7 +812,7 @@ __global__ __launch_bounds__(1024) void me_fast_kernel(SearchArgs p, QsadGeom g)
           for (int i = 0; i < B * CW; i++) csq = __builtin_amdgcn_udot4(cb[i], cb[i], csq, false);
           cost = cost - SSD_BIAS + csq;
         }
-        if (p.cost) p.cost[out] = cost;
+        if (jb.cost[it.j]) jb.cost[it.j][out] = cost;
       }
       ti++;
       pass = 0;
@@ -859,19 +878,11 @@ struct FlowCtl {
   uint32_t done[16];   // wave-tasks of the slot's item finished
 };
 
-// Tile of the flow kernel's launch -> (job, tile of that job's rows): jobs
-// are consecutive tile ranges (jb.tile_pre), every job the same frame
-// geometry; a job's planes and records are its own.
+// Tile of the flow kernel's launch -> its item (all dy chunks: one pass).
 template <int B, int K>
 __device__ __forceinline__ Item flow_item(const SearchArgs& p, const QsadGeom& g,
                                           const FlowJobs& jb, int tile) {
-  int j = 0;
-  while (j + 1 < jb.n && jb.tile_pre[j + 1] <= tile) j++;
-  QsadGeom gj = g;
-  gj.row0 = jb.r0[j];
-  Item it = item_of<B, K>(p, gj, tile - jb.tile_pre[j], 0);
-  it.j = j;
-  return it;
+  return job_item<B, K>(p, g, jb, tile, 0);
 }
 
 // Single-wave LDS DMA of one flow item (the aligned path): tile rows and cur
@@ -1542,12 +1553,14 @@ static int cu_count() {
   return cus;
 }
 
-hipError_t launch_fast(const SearchArgs& p, QsadGeom g, int K, int row0, int nrows,
-                       hipStream_t stream) {
-  if (nrows <= 0) return hipSuccess;
-  g.row0 = row0;
-  g.nrows = nrows;
-  const int ntiles = g.wg_per_row * nrows;
+// One item-kernel launch over the job table jb (full-height rows and h = B/2
+// bottom rows; every job the geometry g was planned for).
+static hipError_t launch_fast(const SearchArgs& p, QsadGeom g, int K, const FlowJobs& jb,
+                              hipStream_t stream) {
+  const int ntiles = jb.tile_pre[jb.n];
+  if (ntiles <= 0) return hipSuccess;
+  g.row0 = 0;
+  g.nrows = 0;  // per job (jb.r0, jb.tile_pre)
   dim3 block((unsigned)g.threads);
 // PP > 0: the instance with that compile-time tile pitch (row addresses in the
 // ds_read2 offset fields), taken when the plan has exactly that pitch.
@@ -1558,7 +1571,7 @@ hipError_t launch_fast(const SearchArgs& p, QsadGeom g, int K, int row0, int nro
     if (e_ != hipSuccess) return e_;                                                       \
     const int res = resident_wgs(fn, g.threads, g.lds);                                    \
     const int nwg = ntiles < res * cu_count() ? ntiles : res * cu_count();                 \
-    hipLaunchKernelGGL((me_fast_kernel<CC, BB, KK, PP>), dim3((unsigned)nwg), block, g.lds, stream, p, g); \
+    hipLaunchKernelGGL((me_fast_kernel<CC, BB, KK, PP>), dim3((unsigned)nwg), block, g.lds, stream, p, g, jb); \
     return hipGetLastError();                                                              \
   }
 #define ME_FAST_CASE(CC, BB, KK) ME_FAST_CASE_P(CC, BB, KK, 0)
@@ -1647,10 +1660,9 @@ static bool cached_flow_plan(const SearchArgs& p, QsadGeom* g) {
   return e.ok;
 }
 
-// One flow-kernel launch over jobs [0, n) (full-height rows and h = B/2
-// bottom rows only; n <= MAX_JOBS).
-static hipError_t launch_flow(const SearchArgs& p, QsadGeom g, const SearchJob* jobs, int n,
-                              hipStream_t stream) {
+// The job table of jobs [0, n) (n <= MAX_JOBS; rows [r0, r1) each, already
+// cut to what the kernel takes), wg_per_row tiles per block row.
+static FlowJobs job_table(const SearchArgs& p, int wg_per_row, const SearchJob* jobs, int n) {
   FlowJobs jb;
   jb.n = 0;
   jb.tile_pre[0] = 0;
@@ -1670,8 +1682,16 @@ static hipError_t launch_flow(const SearchArgs& p, QsadGeom g, const SearchJob* 
     jb.cur[j] = J.cur;
     jb.mv[j] = J.mv;
     jb.cost[j] = J.cost;
-    jb.tile_pre[j + 1] = jb.tile_pre[j] + g.wg_per_row * (J.r1 - J.r0);
+    jb.tile_pre[j + 1] = jb.tile_pre[j] + wg_per_row * (J.r1 - J.r0);
   }
+  return jb;
+}
+
+// One flow-kernel launch over jobs [0, n) (full-height rows and h = B/2
+// bottom rows only; n <= MAX_JOBS).
+static hipError_t launch_flow(const SearchArgs& p, QsadGeom g, const SearchJob* jobs, int n,
+                              hipStream_t stream) {
+  const FlowJobs jb = job_table(p, g.wg_per_row, jobs, n);
   const int ntiles = jb.tile_pre[jb.n];
   if (ntiles <= 0) return hipSuccess;
   g.row0 = 0;
@@ -1731,7 +1751,8 @@ static hipError_t launch_items(const SearchArgs& p, hipStream_t stream, int* use
   int K = 0;
   if (!cached_plan(p, &g, &K)) return launch_generic(p, 0, p.nbx, r0, r1 - r0, stream);
   const int rq1 = qsad_rows_end(p, r1);
-  hipError_t e = launch_fast(p, g, K, r0, rq1 - r0, stream);
+  const SearchJob J{p.ref, p.ref_row0, p.cur, p.cur_row0, r0, rq1, p.mv, p.cost};
+  hipError_t e = launch_fast(p, g, K, job_table(p, g.wg_per_row, &J, 1), stream);
   if (e != hipSuccess) return e;
   if (used_fast) *used_fast = 1;
   if (rq1 < r1) {
@@ -1797,6 +1818,54 @@ static bool launch_flow_jobs(const SearchArgs& base, const SearchJob* jobs, int 
   return true;
 }
 
+// Alignment class of a job's planes (the item planner's key, cached_plan).
+static int align_class(const SearchArgs& p, const uint8_t* ref, const uint8_t* cur) {
+  return ((p.stride % 4 == 0) && ((uintptr_t)ref % 4 == 0) && ((uintptr_t)cur % 4 == 0)) |
+         (((p.stride % 16 == 0) && ((uintptr_t)ref % 16 == 0)) << 1);
+}
+
+// VALU jobs the item kernel takes (SAD, or SSD off the matrix cores) in one
+// launch per MAX_JOBS: per-job launches each paid the persistent grid's fill
+// and drain (8 stripes of a 4K frame: 1.165 ms against 1.047 for the frame).
+// Returns false (nothing launched) when the jobs' planes differ in alignment
+// class or the item kernel does not take the shape.
+static bool launch_item_jobs(const SearchArgs& base, const SearchJob* jobs, int n,
+                             hipStream_t stream, hipError_t* err) {
+  *err = hipSuccess;
+  if (n < 2 || (base.cost_kind != COST_SAD && base.cost_kind != COST_SSD)) return false;
+  const int ac = align_class(base, jobs[0].ref, jobs[0].cur);
+  int rows = 0;
+  for (int i = 0; i < n; i++) {
+    rows += jobs[i].r1 - jobs[i].r0;
+    if (align_class(base, jobs[i].ref, jobs[i].cur) != ac) return false;
+  }
+  SearchArgs probe = job_args(base, jobs[0]);
+  probe.block_row_begin = 0;
+  probe.block_row_end = rows;  // the planner counts tiles over every job's rows
+  QsadGeom g;
+  int K = 0;
+  if (!cached_plan(probe, &g, &K)) return false;
+  for (int i0 = 0; i0 < n && *err == hipSuccess; i0 += MAX_JOBS) {
+    const int m = n - i0 < MAX_JOBS ? n - i0 : MAX_JOBS;
+    SearchJob fj[MAX_JOBS];
+    for (int i = 0; i < m; i++) {
+      fj[i] = jobs[i0 + i];
+      fj[i].r1 = qsad_rows_end(base, fj[i].r1);
+    }
+    *err = launch_fast(base, g, K, job_table(base, g.wg_per_row, fj, m), stream);
+  }
+  // the rows and columns the item kernel leaves, job by job
+  for (int i = 0; i < n && *err == hipSuccess; i++) {
+    const SearchArgs q = job_args(base, jobs[i]);
+    const int rq1 = qsad_rows_end(base, jobs[i].r1);
+    if (rq1 < jobs[i].r1) *err = launch_generic(q, 0, g.nbx_full, rq1, jobs[i].r1 - rq1, stream);
+    if (*err == hipSuccess && g.nbx_full < base.nbx)
+      *err = launch_generic(q, g.nbx_full, base.nbx - g.nbx_full, jobs[i].r0,
+                            jobs[i].r1 - jobs[i].r0, stream);
+  }
+  return true;
+}
+
 static hipError_t launch_valu(const SearchArgs& p, hipStream_t stream, int* used_fast) {
   if (p.block_row_end <= p.block_row_begin) return hipSuccess;
   const SearchJob J{p.ref, p.ref_row0, p.cur, p.cur_row0, p.block_row_begin, p.block_row_end, p.mv, p.cost};
@@ -1811,6 +1880,10 @@ static hipError_t launch_valu(const SearchArgs& p, hipStream_t stream, int* used
 hipError_t launch_jobs(const SearchArgs& base, const SearchJob* jobs, int n, hipStream_t stream) {
   hipError_t e;
   if (n > 1 && launch_flow_jobs(base, jobs, n, stream, &e)) return e;
+  // SSD jobs the matrix cores take go one by one (their prepass planes are per search)
+  MfmaGeom mg;
+  const bool mfma = base.cost_kind == COST_SSD && base.scratch && plan_mfma_ssd(job_args(base, jobs[0]), &mg);
+  if (n > 1 && !mfma && launch_item_jobs(base, jobs, n, stream, &e)) return e;
   for (int i = 0; i < n; i++) {
     if (jobs[i].r1 <= jobs[i].r0) continue;
     e = launch_search(job_args(base, jobs[i]), stream, nullptr);

@@ -9,11 +9,15 @@ library communicator), K back-to-back steps of
   prepared_search+libgather  search + me_gather_device on the same stream
                              (bench.py's direct path, --no-graph)
   graph_search               the search replayed from a captured hipGraph
-  graph_search+libgather     search + gather in one graph (bench.py's default)
+  graph_search+libgather     search + gather in one graph (bench.py --graph)
+  batchF_search              the rank's stripes of F frames (stripe (rank + f) % N
+                             of frame f) in one me_search_stripes_device call
+  batchF_search+libgather    ... and one gather of their records (bench.py's step)
 and prints one JSON line per case: wall us per step, host enqueue us per step
-and HIP-event us per step; then the gathered records' parity.
+and HIP-event us per step (batch cases: also per frame); then the gathered
+records' parity.
 
-  python tools/step_overhead.py [--config 1080p] [--ways 8] [--rank 1] [--steps 2000]
+  python tools/step_overhead.py [--config 1080p] [--ways 8] [--rank 1] [--steps 2000] [--frames 8]
 """
 from __future__ import annotations
 
@@ -35,6 +39,7 @@ def main():
     ap.add_argument("--rank", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--cost", default="sad")
+    ap.add_argument("--frames", type=int, default=8)
     a = ap.parse_args()
     import torch
     import bench
@@ -62,7 +67,7 @@ def main():
     pg = [eng.prepared_gather(recs[k], flat[k]) for k in range(2)]
     state = {"i": 0}
 
-    def run(name, fn, steps):
+    def run(name, fn, steps, frames=1):
         for _ in range(50):
             fn()
         torch.cuda.synchronize()
@@ -75,12 +80,14 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         wall = time.perf_counter() - t0
-        print(json.dumps({"case": name, "config": a.config, "cost": a.cost, "ways": a.ways,
-                          "rank": a.rank, "block_rows": st.row_end - st.row_begin,
-                          "steps": steps, "wall_us_per_step": wall / steps * 1e6,
-                          "host_enqueue_us_per_step": t_host / steps * 1e6,
-                          "gpu_event_us_per_step": e0.elapsed_time(e1) / steps * 1e3}),
-              flush=True)
+        rec = {"case": name, "config": a.config, "cost": a.cost, "ways": a.ways,
+               "rank": a.rank, "block_rows": st.row_end - st.row_begin, "frames": frames,
+               "steps": steps, "wall_us_per_step": wall / steps * 1e6,
+               "host_enqueue_us_per_step": t_host / steps * 1e6,
+               "gpu_event_us_per_step": e0.elapsed_time(e1) / steps * 1e3}
+        if frames > 1:
+            rec["wall_us_per_frame"] = rec["wall_us_per_step"] / frames
+        print(json.dumps(rec), flush=True)
 
     def alternate(calls):
         def step():
@@ -97,9 +104,31 @@ def main():
     gg = [eng.capture(stream, lambda k=k: (ps[k](), pg[k]())) for k in range(2)]
     run("graph_search+libgather", alternate([(gg[0].prepared(stream),),
                                              (gg[1].prepared(stream),)]), a.steps)
+    # bench.py's step: the rank's stripes of F frames in one call + one gather
+    F = a.frames
+    stripes = shard.plan(w, h, blk, span, a.ways)
+    own = [stripes[(a.rank + f) % a.ways] for f in range(F)]
+    mb = stripes[0].max_blocks
+    ref_b = torch.zeros((F, max(o.ref_y1 - o.ref_y0 for o in own), w), dtype=torch.uint8, device=dev)
+    cur_b = torch.zeros((F, max(o.cur_y1 - o.cur_y0 for o in own), w), dtype=torch.uint8, device=dev)
+    for f, o in enumerate(own):
+        ref_b[f, :o.ref_y1 - o.ref_y0] = torch.from_numpy(ref[o.ref_y0:o.ref_y1].copy())
+        cur_b[f, :o.cur_y1 - o.cur_y0] = torch.from_numpy(cur[o.cur_y0:o.cur_y1].copy())
+    brecs = [torch.zeros((2, F * mb), dtype=torch.int32, device=dev) for _ in range(2)]
+    bflat = [torch.empty((1,) + tuple(r.shape), dtype=r.dtype, device=dev) for r in brecs]
+    bmvs = [r[0].view(torch.int16).view(F * mb, 2) for r in brecs]
+    bps = [eng.prepared_stripes_search(
+        w, h, blk, span, a.cost,
+        [(ref_b[f], o.ref_y0, cur_b[f], o.cur_y0, o.row_begin, o.row_end, bmvs[k][f * mb:],
+          brecs[k][1][f * mb:]) for f, o in enumerate(own)], stride=w) for k in range(2)]
+    bpg = [eng.prepared_gather(brecs[k], bflat[k]) for k in range(2)]
+    run(f"batch{F}_search", lambda: bps[0](), max(a.steps // F, 50), F)
+    run(f"batch{F}_search+libgather", alternate([(bps[0], bpg[0]), (bps[1], bpg[1])]),
+        max(a.steps // F, 50), F)
     torch.cuda.synchronize()
     eng.device_check()
     ok = all(torch.equal(flat[k][0], recs[k]) for k in range(2))
+    ok = ok and all(torch.equal(bflat[k][0], brecs[k]) for k in range(2))
     print(json.dumps({"case": "libgather_parity", "equal": ok}), flush=True)
     eng.close()
 
