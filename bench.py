@@ -650,12 +650,13 @@ def main():
     # VALU work: the exact abs-diff count (w*h of each block, not B*B).
     # Stripe mode: the frame's work / N against the slowest rank's kernel time.
     # A launch searches the step's F frames (F stripes in stripe mode).
-    # Frames mode: the step's F frames go out as launches of one frame each
-    # (launch_flow_jobs groups about one LDS ring of tiles per launch, and every
-    # BASELINE frame is more than half a ring; SSD and the item kernel launch per
-    # job), so a launch is one frame: its bytes over kern_ms / F.  Stripe mode:
-    # the rank's F stripes (one ring of tiles per launch at N = 8, a few
-    # launches at N = 2, 4) are priced as a whole step.
+    # Priced per frame in frames mode: the bytes of one frame over kern_ms / F.
+    # At 1080p SAD (the headline) a launch is one frame (launch_flow_jobs puts
+    # about one LDS ring of tiles in a launch, and a 1080p frame is more than
+    # half a ring); 4K / 8K SAD batches share one item-kernel launch and SSD
+    # launches per frame, so the rate is per frame throughout, and roofline.traffic
+    # (tools/profile_all.sh, one frame per step) is per frame too.  Stripe mode:
+    # the rank's F stripes are priced as a whole step.
     if mode == "frames":
         alg_bytes = 2 * w * h + 8 * nb
         launch_ms = kern_ms / F
@@ -695,11 +696,12 @@ def main():
                    "candidates_per_frame": cands_frame, "blocks_per_frame": nb,
                    "frames_per_step": F, "parallelism": f"{mode}{world}"},
         "kernel_ms": kern_ms,
-        "launch_ms": launch_ms,
+        "kernel_ms_per_unit": launch_ms,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_per_search": traffic_search,
-                     "algorithmic_bytes_per_launch": alg_bytes,
+                     "algorithmic_bytes": alg_bytes,
+                     "per": "frame" if mode == "frames" else "rank step",
                      "valu": {"achieved_absdiff_per_s": absdiffs / (kern_ms / 1e3),
                               "peak_absdiff_per_s": VALU_PEAK_ABSDIFF,
                               "frac": absdiffs / (kern_ms / 1e3) / VALU_PEAK_ABSDIFF}},
@@ -720,7 +722,7 @@ def main():
                             "note": "useful int8 ops (2*w*h per candidate) over the whole search "
                                     "(S2 prepass + MFMA kernel); dense i8 peak",
                             "hbm": {k: hbm[k] for k in ("achieved", "peak", "unit", "frac",
-                                                        "algorithmic_bytes_per_launch")}}
+                                                        "algorithmic_bytes", "per")}}
     if rank == 0 and world == 1 and mode == "frames" and F > 1:
         # the same search one frame per launch (me_full_search_device), for
         # comparison: the batch's only difference is launches per frame

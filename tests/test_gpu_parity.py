@@ -378,9 +378,10 @@ def test_stripes_of_multi_gpu_splits(engine, span):
 @pytest.mark.parametrize("cost,blk,span,w,h,ways", [
     ("sad", 16, 32, 1920, 1080, 8),   # flow kernel, one launch for the batch (h = 8 bottom row)
     ("sad", 16, 32, 1920, 1080, 1),   # whole frames batched
-    ("sad", 16, 16, 1000, 700, 3),    # partial right column + h = 12 bottom row: per-frame kernels
+    ("sad", 16, 16, 1000, 700, 3),    # item kernel over the batch; generic kernel for the
+                                      # partial right column and the h = 12 bottom row
     ("ssd", 16, 32, 1920, 1080, 4),   # matrix cores, frame by frame
-    ("sad", 8, 24, 640, 360, 2),      # 8x8 item kernel, frame by frame
+    ("sad", 8, 24, 640, 360, 2),      # 8x8 item kernel, one launch for the batch
 ])
 def test_batch_search_equals_per_frame(engine, cost, blk, span, w, h, ways):
     """me_full_search_batch_device: F stripes (or whole frames) of different
@@ -441,7 +442,7 @@ def test_batch_search_argument_checks(engine):
 @pytest.mark.parametrize("cost,blk,span,w,h,ways", [
     ("sad", 16, 32, 1920, 1080, 8),   # flow kernel: one launch for stripes of different rows
     ("sad", 16, 32, 1920, 1080, 4),
-    ("sad", 16, 16, 1000, 700, 3),    # per-job item / generic kernels
+    ("sad", 16, 16, 1000, 700, 3),    # item kernel over the jobs + generic leftovers
     ("ssd", 16, 32, 1920, 1080, 8),   # matrix cores, job by job
 ])
 def test_stripe_jobs_of_different_rows(engine, cost, blk, span, w, h, ways):
@@ -476,4 +477,54 @@ def test_stripe_jobs_of_different_rows(engine, cost, blk, span, w, h, ways):
             msg = f"{cost} {w}x{h} rank {r} frame {f} rows {st.row_begin}:{st.row_end}"
             np.testing.assert_array_equal(job[6].cpu().numpy(), omv, err_msg=msg)
             np.testing.assert_array_equal(job[7].cpu().numpy().view(np.uint32), oco, err_msg=msg)
+    engine.device_check()
+
+
+@pytest.mark.parametrize("cfg,blk,span,ways,F", [
+    ("4k", 16, 64, 8, 8),   # bench.py's 4K 8-way step: one item-kernel launch, pitch-272 instance
+    ("4k", 16, 64, 1, 3),   # whole 4K frames batched (dynamic tile pulls over the batch)
+    ("8k", 8, 128, 2, 2),   # 8x8 strip walk per job (>= 32 tiles wide and 32 rows tall)
+])
+def test_item_kernel_jobs_equal_single_searches(engine, cfg, blk, span, ways, F):
+    """The item kernel over a job table (me_search_stripes_device with bench.py's
+    rotated step: job f = stripe (r + f) % N of frame f) equals one
+    me_full_search_device per frame on the same rows, bit for bit; the
+    single-frame searches are pinned by the full-frame hashes
+    (tests/test_gpu_fullframe.py)."""
+    import torch
+    from motionestimation_amd import shard
+    base_ref, base_cur = synth.named_pair(cfg)
+    h, w = base_ref.shape
+    nb = me.num_blocks(w, h, blk)
+    frames = [(np.roll(base_ref, 37 * f, axis=1), np.roll(base_cur, 37 * f, axis=1))
+              for f in range(F)]
+    want = []
+    for r, c in frames:
+        rt, ct = torch.from_numpy(r).cuda(), torch.from_numpy(c).cuda()
+        mv = torch.empty((nb, 2), dtype=torch.int16, device="cuda")
+        co = torch.empty(nb, dtype=torch.int32, device="cuda")
+        engine.full_search_device(rt, ct, blk, span, "sad", mv, co)
+        torch.cuda.synchronize()
+        want.append((mv.cpu().numpy(), co.cpu().numpy()))
+        del rt, ct
+    plan = shard.plan(w, h, blk, span, ways)
+    for rank in sorted({0, ways - 1}):
+        own = [plan[(rank + f) % ways] for f in range(F)]
+        jobs, keep = [], []
+        for f, st in enumerate(own):
+            r, c = frames[f]
+            rt = torch.from_numpy(r[st.ref_y0:st.ref_y1].copy()).cuda()
+            ct = torch.from_numpy(c[st.cur_y0:st.cur_y1].copy()).cuda()
+            mv = torch.full((st.nblocks, 2), -7, dtype=torch.int16, device="cuda")
+            co = torch.zeros(st.nblocks, dtype=torch.int32, device="cuda")
+            jobs.append((rt, st.ref_y0, ct, st.cur_y0, st.row_begin, st.row_end, mv, co))
+            keep.append((st, mv, co))
+        engine.search_stripes_device(w, h, blk, span, "sad", jobs)
+        torch.cuda.synchronize()
+        for f, (st, mv, co) in enumerate(keep):
+            b0, b1 = st.row_begin * st.nbx, st.row_end * st.nbx
+            msg = f"{cfg} {ways}-way rank {rank} frame {f} rows {st.row_begin}:{st.row_end}"
+            np.testing.assert_array_equal(mv.cpu().numpy(), want[f][0][b0:b1], err_msg=msg)
+            np.testing.assert_array_equal(co.cpu().numpy(), want[f][1][b0:b1], err_msg=msg)
+        del jobs, keep
     engine.device_check()
