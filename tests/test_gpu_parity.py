@@ -528,3 +528,52 @@ def test_item_kernel_jobs_equal_single_searches(engine, cfg, blk, span, ways, F)
             np.testing.assert_array_equal(co.cpu().numpy(), want[f][1][b0:b1], err_msg=msg)
         del jobs, keep
     engine.device_check()
+
+
+def test_random_job_tables_equal_per_job_searches(engine):
+    """Property: me_search_stripes_device over a random job table (random row
+    ranges of random frames, empty jobs, more jobs than one launch holds)
+    equals one me_full_search_stripe_device call per job, for every kernel
+    family the shapes reach (flow, item, generic, matrix cores)."""
+    import torch
+    rng = np.random.default_rng(2024)
+    shapes = [  # cost, B, S, W, H
+        ("sad", 16, 32, 1920, 1080),   # flow kernel
+        ("sad", 16, 16, 1000, 700),    # item kernel + generic leftovers
+        ("sad", 8, 24, 640, 360),      # 8x8 item kernel
+        ("ssd", 16, 32, 640, 480),     # matrix cores, job by job
+        ("ssd", 8, 12, 330, 203),      # 8x8 matrix cores + partial column and row
+        ("sad", 12, 9, 400, 300),      # generic kernel only
+    ]
+    for cost, blk, span, w, h in shapes:
+        nby = (h + blk - 1) // blk
+        nbx = (w + blk - 1) // blk
+        n = int(rng.integers(2, 21))
+        pairs = [synth.frame_pair(w, h, int(rng.integers(1, 1 << 30)), int(rng.integers(-6, 7)),
+                                  int(rng.integers(-6, 7))) for _ in range(min(n, 4))]
+        jobs, singles = [], []
+        for j in range(n):
+            r, c = pairs[j % len(pairs)]
+            r0 = int(rng.integers(0, nby))
+            r1 = r0 if j == 1 else int(rng.integers(r0 + 1, nby + 1))  # job 1 empty
+            y0, y1 = max(r0 * blk - span, 0), min(r1 * blk + span, h)
+            ref_t = torch.from_numpy(r[y0:y1].copy()).cuda() if y1 > y0 else torch.zeros(
+                (1, w), dtype=torch.uint8, device="cuda")
+            cur_t = torch.from_numpy(c[r0 * blk:min(r1 * blk, h)].copy()).cuda() if r1 > r0 else \
+                torch.zeros((1, w), dtype=torch.uint8, device="cuda")
+            nblk = (r1 - r0) * nbx
+            mv = torch.full((max(nblk, 1), 2), -9, dtype=torch.int16, device="cuda")
+            co = torch.zeros(max(nblk, 1), dtype=torch.int32, device="cuda")
+            jobs.append((ref_t, y0, cur_t, r0 * blk, r0, r1, mv, co))
+            mv1, co1 = mv.clone(), co.clone()
+            if r1 > r0:
+                engine.search_stripe_device(ref_t, y0, cur_t, r0 * blk, w, h, blk, span, cost,
+                                            r0, r1, mv1, co1)
+            singles.append((mv1, co1))
+        engine.search_stripes_device(w, h, blk, span, cost, jobs)
+        torch.cuda.synchronize()
+        for j, ((_, _, _, _, r0, r1, mv, co), (mv1, co1)) in enumerate(zip(jobs, singles)):
+            msg = f"{cost} B{blk} S{span} {w}x{h} job {j}/{n} rows {r0}:{r1}"
+            np.testing.assert_array_equal(mv.cpu().numpy(), mv1.cpu().numpy(), err_msg=msg)
+            np.testing.assert_array_equal(co.cpu().numpy(), co1.cpu().numpy(), err_msg=msg)
+    engine.device_check()
