@@ -651,12 +651,11 @@ def main():
     # Stripe mode: the frame's work / N against the slowest rank's kernel time.
     # A launch searches the step's F frames (F stripes in stripe mode).
     # Priced per frame in frames mode: the bytes of one frame over kern_ms / F.
-    # At 1080p SAD (the headline) a launch is one frame (launch_flow_jobs puts
-    # about one LDS ring of tiles in a launch, and a 1080p frame is more than
-    # half a ring); 4K / 8K SAD batches share one item-kernel launch and SSD
-    # launches per frame, so the rate is per frame throughout, and roofline.traffic
-    # (tools/profile_all.sh, one frame per step) is per frame too.  Stripe mode:
-    # the rank's F stripes are priced as a whole step.
+    # SAD batches share one launch (1080p: the flow kernel's job table; 4K / 8K:
+    # the item kernel's), so a launch's bytes over its duration give the same
+    # rate; SSD launches per frame.  roofline.traffic (tools/profile_all.sh, one
+    # frame per step) is per frame too.  Stripe mode: the rank's F stripes are
+    # priced as a whole step.
     if mode == "frames":
         alg_bytes = 2 * w * h + 8 * nb
         launch_ms = kern_ms / F

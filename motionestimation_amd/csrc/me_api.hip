@@ -65,6 +65,17 @@ static Tuning read_tuning() {
   env_int("ME_FLOW_SLOTS", 2, 16, &t.flow_slots);
   env_int("ME_PRIO", 0, 1, &t.prio);
   env_int("ME_STRIP", 0, 64, &t.strip);
+  env_int("ME_FAIR", 0, 3, &t.fair);
+  env_int("ME_FLOW_ONE", 0, 1, &t.flow_one);
+  if (const char* e = getenv("ME_FAIR_T")) {
+    int lo = 0, hi = 0;
+    if (sscanf(e, "%d,%d", &lo, &hi) == 2 && lo >= 1 && lo <= hi && hi <= 255) {
+      t.fair_lo = lo;
+      t.fair_hi = hi;
+    } else {
+      fprintf(stderr, "me_hip: ignoring ME_FAIR_T=%s (lo,hi with 1 <= lo <= hi <= 255)\n", e);
+    }
+  }
   return t;
 }
 const Tuning& tuning() {

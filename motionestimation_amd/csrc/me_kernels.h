@@ -68,6 +68,10 @@ struct QsadGeom {
   int dyn_tiles;   // dynamic tile pulls when tiles >= dyn_tiles * workgroups (0: never)
   int flow_slots;  // me_flow_kernel: LDS ring slots (0: the persistent item kernel)
   int prio;        // waves issuing staging raise their issue priority (s_setprio) meanwhile
+  int fair;        // me_flow_kernel: lo | hi << 8 | mode << 16 (0: off): a wave whose
+                   // wave-task others have overtaken by >= lo / hi pulls raises its
+                   // issue priority to 1 / 2 (checked every 4 rows; 8 / 16 by
+                   // default) in launches with slot refills (mode 1)
 };
 
 // A search job: block rows [r0, r1) of one frame (or row stripe), its planes
@@ -100,8 +104,8 @@ struct FlowJobs {
 };
 
 // Search every job (geometry, cost and scratch from base): SAD jobs the flow
-// kernel takes share launches (at most one LDS ring of tiles per CU each),
-// everything else runs job by job through launch_search.
+// kernel takes share one launch (up to MAX_JOBS jobs), VALU jobs of the item
+// kernel likewise, everything else runs job by job through launch_search.
 hipError_t launch_jobs(const SearchArgs& base, const SearchJob* jobs, int n, hipStream_t stream);
 
 // Matrix-core SSD path (me_mfma.hip): B = 16, full-height rows [row0, row0 +

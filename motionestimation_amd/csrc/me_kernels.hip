@@ -197,10 +197,16 @@ __device__ __forceinline__ void pin_rows32(uint32_t (&acc)[K]) {
 // PC > 0: the pitch is that compile-time constant, and the rows of a group of
 // RG share one base address (the row offset goes into the ds_read2 offset
 // fields, <= 1020 bytes): one address add per group instead of per row.
-template <int B, int K, int H, int PC = 0>
+// HK > 0: hook() runs at the start of every HK-th window row (the flow kernel's
+// issue-priority check).
+struct NoHook {
+  __device__ void operator()() const {}
+};
+template <int B, int K, int H, int PC = 0, int HK = 0, typename Hook = NoHook>
 __device__ __forceinline__ void qsad_lane(const uint8_t* __restrict__ tile, int pitch,
                                           uint32_t buf_off, int lrow, int w0,
-                                          const uint32_t (&c)[B][B / 4], uint64_t (&acc)[K]) {
+                                          const uint32_t (&c)[B][B / 4], uint64_t (&acc)[K],
+                                          Hook hook = Hook{}) {
   constexpr int CW = B / 4;
   constexpr int NR = K + H - 1;
   constexpr int RG = PC > 0 ? ((1020 - 4 * CW) / PC + 1 < 8 ? (1020 - 4 * CW) / PC + 1 : 8) : 1;
@@ -233,6 +239,10 @@ __device__ __forceinline__ void qsad_lane(const uint8_t* __restrict__ tile, int 
     constexpr int yy = decltype(YY)::value;
     // one segment per window row: next row's loads, then this row's qsads.
     __builtin_amdgcn_sched_barrier(0);
+    if constexpr (HK > 0 && yy > 0 && yy % HK == 0) {
+      hook();
+      __builtin_amdgcn_sched_barrier(0);
+    }
     if constexpr (yy + 1 < NR) {
       if constexpr (PC > 0) {
         constexpr int nr = yy + 1;
@@ -1010,6 +1020,7 @@ __global__ __launch_bounds__(1024) void me_flow_kernel(SearchArgs p, QsadGeom g,
       }
     }
     if (kc >= nitems) break;
+    if (g.fair) __builtin_amdgcn_s_setprio(0);
     const int slot = kc % NB;
     // Bounded wait (the ordering argument above says it ends; the bound keeps a
     // broken invariant from hanging the GPU).  An expired wait is reported:
@@ -1077,11 +1088,34 @@ __global__ __launch_bounds__(1024) void me_flow_kernel(SearchArgs p, QsadGeom g,
     const int jt = gi < K ? gi : K - 1;
     const uint32_t toff = tile_off + (uint32_t)((lc * K + jt) * g.pitch + b * B + 2 * S);
     uint32_t tsad = 0;
+    // Fairness: the SIMD arbiter issues the oldest waves first, so a young
+    // wave's wave-task lags while older waves run through later items (single
+    // 1080p frames: per SIMD one wave ran ~6 wave-tasks, two ran 1 each), and
+    // the slot refill that waits for it stalls every wave behind the ring.
+    // Every 4 rows the wave compares its task with the pull counter and raises
+    // its priority once lo / hi later tasks have been pulled (g.fair; back to
+    // 0 at its next pull).  Only in launches with refills: without them (a
+    // single 1080p frame, every tile staged at the start) the oldest-first
+    // order ends the launch sooner (70.4 vs 74.7 us with the check on,
+    // profiles/r03ad_*).  Tuning build, g.fair bits 16-17 (ME_FAIR): 2 = only
+    // on items whose slot still gets a refill, 3 = on every item.
+    const int fmode = g.fair >> 16;
+    const bool fair = g.fair != 0 && (fmode == 3 || (fmode == 2 ? kc + NB < nitems : nitems > NB));
+    const int lag1 = g.fair & 255, lag2 = (g.fair >> 8) & 255;
+    auto lag_check = [&]() {
+      if (fair) {
+        const int nx = __builtin_amdgcn_readfirstlane(
+            (int)__hip_atomic_load(&ctl->next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        const int lag = nx - (int)q;
+        if (lag >= lag2) __builtin_amdgcn_s_setprio(2);
+        else if (lag >= lag1) __builtin_amdgcn_s_setprio(1);
+      }
+    };
     if (it.h == B) {
-      qsad_lane<B, K, B, PC>(smem, g.pitch, tile_off, lc * K, w0, c, acc);
+      qsad_lane<B, K, B, PC, 4>(smem, g.pitch, tile_off, lc * K, w0, c, acc, lag_check);
       if (g.fold) tsad = tail_sad<B, B>(smem, g.pitch, toff, c);
     } else {
-      qsad_lane<B, K, B / 2, PC>(smem, g.pitch, tile_off, lc * K, w0, c, acc);
+      qsad_lane<B, K, B / 2, PC, 4>(smem, g.pitch, tile_off, lc * K, w0, c, acc, lag_check);
       if (g.fold) tsad = tail_sad<B, B / 2>(smem, g.pitch, toff, c);
     }
     const int dxg = 4 * gi - S - it.a;
@@ -1366,6 +1400,7 @@ bool plan_fast(const SearchArgs& p, QsadGeom* g, int* k_out) {
       if (nb > 1 && (uint32_t)(((uint64_t)x * m) >> 32) != x / nb) return false;
   }
   g->prio = tu.prio != 0;
+  g->fair = 0;
   g->flow_slots = 0;
   // Wide frames: vertical strips of 16 tiles (8K 8x8: 1,024 pixels plus the
   // window's 2S), so an XCD's contiguous run of the order is a few whole
@@ -1482,6 +1517,9 @@ bool plan_flow(const SearchArgs& p, QsadGeom* g) {
   if (tuning().flow_slots && tuning().flow_slots < best_ns) best_ns = tuning().flow_slots;
   q.flow_slots = best_ns;
   q.prio = tuning().prio != 0;
+  q.fair = tuning().fair != 0
+               ? (tuning().fair_lo | tuning().fair_hi << 8 | (tuning().fair > 1 ? tuning().fair : 1) << 16)
+               : 0;
   q.strip_w = 0;
   q.lds = best_ns * slot + best_ns * q.tb * 8 + (int)sizeof(int) * 40;
   return q.lds <= 160 * 1024;
@@ -1765,10 +1803,13 @@ static hipError_t launch_items(const SearchArgs& p, hipStream_t stream, int* use
 }
 
 // SAD jobs on the flow kernel where its plan (over every job's rows) takes
-// them, in launches of about one LDS ring of tiles per CU each: past the
-// ring, refills under compute starved the waves (8 1080p frames in one
-// launch: 22 % of wave time spinning on unpublished slots, 87 us per frame
-// against 69 for single frames; profiles/r03n_flow_stamps_batch.txt).
+// them, all in one launch (MAX_JOBS jobs per launch).  Past the LDS ring a
+// slot is refilled when its item's last wave-task ends; with the fairness
+// check in the kernel (QsadGeom::fair) that wave-task no longer lags, and one
+// launch of 8 1080p frames takes 62.5-63 us per frame against 71.4 for
+// back-to-back single-frame launches on the same box (without the check:
+// 80.9 us, waves spinning on unpublished slots; profiles/r03ac_fair_sweep.jsonl).
+// Tuning build: ME_FLOW_ONE=0 cuts a batch into launches of about one ring.
 // Returns false (nothing launched) when the flow kernel does not apply.
 static bool launch_flow_jobs(const SearchArgs& base, const SearchJob* jobs, int n, hipStream_t stream,
                              hipError_t* err) {
@@ -1787,7 +1828,7 @@ static bool launch_flow_jobs(const SearchArgs& base, const SearchJob* jobs, int 
   long total = 0;
   for (int i = 0; i < n; i++)
     total += (long)g.wg_per_row * (qsad_rows_end(base, jobs[i].r1) - jobs[i].r0);
-  const long ring = (long)g.flow_slots * cu_count();
+  const long ring = tuning().flow_one != 0 ? (1L << 40) : (long)g.flow_slots * cu_count();
   const long nl = (total + ring - 1) / ring;  // launches of about total / nl tiles
   const long target = nl > 1 ? (total + nl - 1) / nl : total;
   SearchJob fj[MAX_JOBS];

@@ -23,6 +23,10 @@ struct Tuning {
   int flow = -1;          // ME_FLOW=0|1: SAD flow kernel off / allowed (-1 = automatic)
   int flow_slots = 0;     // ME_FLOW_SLOTS=2..16: flow kernel LDS ring slots (0 = automatic)
   int prio = -1;          // ME_PRIO=0|1: staging waves raise their issue priority (-1 = automatic: on)
+  int fair = -1;          // ME_FAIR=0..3: flow-kernel waves behind the pull counter raise their priority: 0 off, 1 in launches
+                          // with refills (automatic), 2 on items whose slot gets a refill, 3 always
+  int fair_lo = 8, fair_hi = 16;  // ME_FAIR_T=lo,hi: the lags (pulls) that raise a wave to priority 1 / 2
+  int flow_one = -1;      // ME_FLOW_ONE=0|1: a batch's flow jobs in launches of one ring / in one launch (-1 = automatic: one)
   int strip = -1;         // ME_STRIP=0..64: item-kernel tile strips (0 = row-major; -1 = automatic)
 };
 
