@@ -9,8 +9,9 @@ resident in HBM before the timed region.
   python bench.py [--gpus N] [--steps K] [--warmup W] [--mode auto|frames|stripe]
                   [--config 1080p|4k|8k] [--cost sad|ssd] [--no-cpu]
 
-A step is a batch of --frames-per-step F frames (default 8), searched in one
-launch per rank (me_full_search_batch_device).
+A step is a batch of --frames-per-step F frames (default 16), searched in one
+launch per rank (me_full_search_batch_device; in stripe mode the rank's F
+stripes, me_search_stripes_device).
 --mode stripe (the default for N > 1, north_star's split): the step's F frames
   are each split into cost-balanced block-row stripes, one per rank, each rank
   holding only its stripes + S-row ref halos; the per-stripe MV records of all
@@ -46,6 +47,7 @@ sys.path.insert(0, REPO)
 
 METRIC = "16×16 SAD candidates/sec at 1080p ±32; achieved HBM GB/s vs roofline"
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
+MAX_JOBS = 32                # jobs per kernel launch (csrc/me_kernels.h): SAD batches share launches
 VALU_PEAK_ABSDIFF = 157.3e12  # 256 CU x 64 lanes x 2.4 GHz x 4 |a-b| per op (measured: profiles/)
 I8_PEAK_TOPS = 5000.0         # MI355X_MICROARCH.md: dense I8 MFMA = 2x BF16 (2.5 PF) per clock
 CONFIGS = {  # name -> (synth config, block, range)
@@ -72,12 +74,14 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16,
                     help="threads of the main CPU-baseline leg (the GPU box's CPU share)")
     ap.add_argument("--no-4k", action="store_true", help="skip the nested stripe_4k record")
+    ap.add_argument("--no-single", action="store_true",
+                    help="skip the single_frame record (one frame per launch, for comparison)")
     ap.add_argument("--graph", action="store_true",
                     help="stripe mode over RCCL: replay search + gather as one captured hipGraph "
                          "per step instead of two enqueues (measured slower on one GPU)")
     ap.add_argument("--ramp-ms", type=float, default=100.0,
                     help="untimed steps for this long before the W warmup steps (GPU clock ramp)")
-    ap.add_argument("--frames-per-step", type=int, default=8,
+    ap.add_argument("--frames-per-step", type=int, default=16,
                     help="frames searched per step: one batched launch per rank "
                          "(me_full_search_batch_device) and, in stripe mode, one gather per step")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
@@ -649,16 +653,17 @@ def main():
     # for the planes that launch covers.
     # VALU work: the exact abs-diff count (w*h of each block, not B*B).
     # Stripe mode: the frame's work / N against the slowest rank's kernel time.
-    # A launch searches the step's F frames (F stripes in stripe mode).
-    # Priced per frame in frames mode: the bytes of one frame over kern_ms / F.
-    # SAD batches share one launch (1080p: the flow kernel's job table; 4K / 8K:
-    # the item kernel's), so a launch's bytes over its duration give the same
-    # rate; SSD launches per frame.  roofline.traffic (tools/profile_all.sh, one
-    # frame per step) is per frame too.  Stripe mode: the rank's F stripes are
-    # priced as a whole step.
+    # Priced per launch of the dominant kernel.  SAD batches share launches of
+    # up to MAX_JOBS (32) frames (1080p: the flow kernel's job table; 4K / 8K:
+    # the item kernel's); SSD launches per frame (prepass + matrix-core kernel).
+    # So a launch holds fpl frames and lasts kern_ms * fpl / F.  Stripe mode:
+    # the rank's F stripes, one launch per step (F <= 32).  roofline.traffic is
+    # the PMC bytes per launch of the same workload at the same F
+    # (tools/profile_all.sh -> profiles/pmc_summary.json).
+    fpl = min(F, MAX_JOBS) if args.cost == "sad" else 1
     if mode == "frames":
-        alg_bytes = 2 * w * h + 8 * nb
-        launch_ms = kern_ms / F
+        alg_bytes = fpl * (2 * w * h + 8 * nb)
+        launch_ms = kern_ms * fpl / F
         absdiffs = F * exact_absdiffs(w, h, blk, span)
     else:
         alg_bytes = sum((o.ref_y1 - o.ref_y0 + o.cur_y1 - o.cur_y0) * w + 8 * o.nblocks
@@ -666,8 +671,8 @@ def main():
         launch_ms = kern_ms
         absdiffs = F * exact_absdiffs(w, h, blk, span) / world
     achieved = alg_bytes / (launch_ms / 1e3) / 1e9
-    tag = f"{args.config}_b{blk}_s{span}_{args.cost}"
-    traffic, traffic_search = load_traffic(tag)
+    tag = f"{args.config}_b{blk}_s{span}_{args.cost}_f{F}"
+    traffic, traffic_search = load_traffic(tag) if mode == "frames" else (None, None)
     line = {
         "metric": METRIC if args.config == "1080p" and args.cost == "sad" else
         f"{blk}x{blk} {args.cost.upper()} candidates/sec at {args.config} +-{span}",
@@ -700,7 +705,9 @@ def main():
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_per_search": traffic_search,
                      "algorithmic_bytes": alg_bytes,
-                     "per": "frame" if mode == "frames" else "rank step",
+                     "per": "launch" if mode == "frames" else "rank step",
+                     "frames_per_launch": fpl if mode == "frames" else F,
+                     "launch_ms": launch_ms,
                      "valu": {"achieved_absdiff_per_s": absdiffs / (kern_ms / 1e3),
                               "peak_absdiff_per_s": VALU_PEAK_ABSDIFF,
                               "frac": absdiffs / (kern_ms / 1e3) / VALU_PEAK_ABSDIFF}},
@@ -721,8 +728,9 @@ def main():
                             "note": "useful int8 ops (2*w*h per candidate) over the whole search "
                                     "(S2 prepass + MFMA kernel); dense i8 peak",
                             "hbm": {k: hbm[k] for k in ("achieved", "peak", "unit", "frac",
-                                                        "algorithmic_bytes", "per")}}
-    if rank == 0 and world == 1 and mode == "frames" and F > 1:
+                                                        "algorithmic_bytes", "per",
+                                                        "frames_per_launch", "launch_ms")}}
+    if rank == 0 and world == 1 and mode == "frames" and F > 1 and not args.no_single:
         # the same search one frame per launch (me_full_search_device), for
         # comparison: the batch's only difference is launches per frame
         line["single_frame"] = single_frame(eng, ref_t[0], cur_t[0], blk, span, args.cost, nb,

@@ -90,7 +90,7 @@ struct SearchJob {
 // The flow kernel's job table (kernel argument): job j owns launch tiles
 // [tile_pre[j], tile_pre[j + 1]).  A batch of frames or stripes (the per-rank
 // step of a multi-GPU split) fills the GPU in one launch.
-constexpr int MAX_JOBS = 16;
+constexpr int MAX_JOBS = 32;
 struct FlowJobs {
   int n;
   int tile_pre[MAX_JOBS + 1];

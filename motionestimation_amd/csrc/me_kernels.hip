@@ -1101,15 +1101,24 @@ __global__ __launch_bounds__(1024) void me_flow_kernel(SearchArgs p, QsadGeom g,
     // on items whose slot still gets a refill, 3 = on every item.
     const int fmode = g.fair >> 16;
     const bool fair = g.fair != 0 && (fmode == 3 || (fmode == 2 ? kc + NB < nitems : nitems > NB));
-    const int lag1 = g.fair & 255, lag2 = (g.fair >> 8) & 255;
-    auto lag_check = [&]() {
-      if (fair) {
-        const int nx = __builtin_amdgcn_readfirstlane(
-            (int)__hip_atomic_load(&ctl->next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-        const int lag = nx - (int)q;
-        if (lag >= lag2) __builtin_amdgcn_s_setprio(2);
-        else if (lag >= lag1) __builtin_amdgcn_s_setprio(1);
-      }
+    // pull-counter values that raise the priority (two SGPRs across the rows)
+    const int lim1 = __builtin_amdgcn_readfirstlane(fair ? (int)q + (g.fair & 255) : 0x7FFFFFFF);
+    const int lim2 = __builtin_amdgcn_readfirstlane(fair ? (int)q + ((g.fair >> 8) & 255) : 0x7FFFFFFF);
+    // The compare and s_setprio sit in one asm block: as C branches they split
+    // the unrolled row loop into basic blocks, and it spilled 41 VGPRs.
+    auto lag_check = [lim1, lim2, ctl]() {
+      const int nx = __builtin_amdgcn_readfirstlane(
+          (int)__hip_atomic_load(&ctl->next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+      asm volatile(
+          "s_cmp_ge_i32 %0, %2\n\t"
+          "s_cbranch_scc0 1f\n\t"
+          "s_setprio 2\n\t"
+          "s_branch 2f\n"
+          "1:\n\t"
+          "s_cmp_ge_i32 %0, %1\n\t"
+          "s_cbranch_scc0 2f\n\t"
+          "s_setprio 1\n"
+          "2:" ::"s"(nx), "s"(lim1), "s"(lim2) : "scc");
     };
     if (it.h == B) {
       qsad_lane<B, K, B, PC, 4>(smem, g.pitch, tile_off, lc * K, w0, c, acc, lag_check);

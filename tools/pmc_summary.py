@@ -78,13 +78,18 @@ for k, v in summary.items():
 bench_tag = None
 cfg = "1080p"
 cost = "sad"
+frames = 16  # bench.py --frames-per-step default
 for i, a in enumerate(args):
     if a == "--config":
         cfg = args[i + 1]
     if a == "--cost":
         cost = args[i + 1]
+    if a == "--frames-per-step":
+        frames = int(args[i + 1])
 blk, span = {"1080p": (16, 32), "4k": (16, 64), "8k": (8, 128)}[cfg]
-bench_tag = f"{cfg}_b{blk}_s{span}_{cost}"
+# keyed like bench.py's lookup: the workload and its frames per step (a SAD
+# launch holds every frame of the step, an SSD launch one frame)
+bench_tag = f"{cfg}_b{blk}_s{span}_{cost}_f{frames}"
 path = os.path.join(PROF, "pmc_summary.json")
 try:
     allsum = json.load(open(path))
