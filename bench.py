@@ -238,25 +238,29 @@ def single_frame(eng, ref_t, cur_t, blk, span, cost, nb, cands_frame, dev, steps
 
 
 def ssd_beside(eng, ref_t, cur_t, blk, span, nb, cands_frame, dev, steps):
-    """The reference's own cost (MSE = SSD / 256) on the same resident frame pair:
-    B = 16 SSD runs on the matrix cores (i8 MFMA).  Reported beside `value`."""
+    """The reference's own cost (MSE = SSD / 256) on the step's resident frame
+    pairs ([F, H, W] stacks): B = 16 SSD runs on the matrix cores (i8 MFMA), the
+    F frames in one batched call (one prepass and one block-major launch).
+    Reported beside `value`; `kernel_ms` is per frame."""
     import torch
-    mv = torch.empty((nb, 2), dtype=torch.int16, device=dev)
-    co = torch.empty(nb, dtype=torch.int32, device=dev)
+    F, h, w = ref_t.shape
+    nby = (h + blk - 1) // blk
+    mv = torch.empty((F * nb, 2), dtype=torch.int16, device=dev)
+    co = torch.empty(F * nb, dtype=torch.int32, device=dev)
+    run = eng.prepared_batch_search(ref_t, 0, cur_t, 0, w, h, blk, span, "ssd", 0, nby, mv, co)
     for _ in range(3):
-        eng.full_search_device(ref_t, cur_t, blk, span, "ssd", mv, co)
+        run()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     e0.record()
     for _ in range(steps):
-        eng.full_search_device(ref_t, cur_t, blk, span, "ssd", mv, co)
+        run()
     e1.record()
     torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / steps
-    h, w = ref_t.shape
+    ms = e0.elapsed_time(e1) / steps / F
     tops = 2.0 * exact_absdiffs(w, h, blk, span) / (ms / 1e3) / 1e12
     return {"value": cands_frame / (ms / 1e3), "unit": "candidates/s", "kernel_ms": ms,
-            "steps": steps, "cost": "ssd (reference MSE argmin, bit-exact)",
+            "steps": steps, "frames_per_step": F, "cost": "ssd (reference MSE argmin, bit-exact)",
             "roofline": {"bound": "mfma", "achieved": tops, "peak": I8_PEAK_TOPS,
                          "unit": "TFLOP/s", "frac": tops / I8_PEAK_TOPS}}
 
@@ -515,6 +519,22 @@ def stripe_record(eng, dev, world, rank, gloo, cfg_name, cost, steps, warmup, nf
             "gather": sr.gather_impl()}
 
 
+def ssd_frames_per_launch(w, h, blk, span, F):
+    """Frames per matrix-core launch pair of an F-frame SSD batch (me_mfma.hip
+    launch_mfma_jobs): B = 16 (block-major kernel, S <= 192) batches as many
+    frames as MAX_JOBS and 1 GiB of prepass planes allow (rp plane + one or two
+    4-byte S2 planes over the rows + 16, 256-byte aligned); 8x8 searches
+    launch per frame."""
+    if blk != 16 or span > 192 or F < 2:
+        return 1
+    rows = h + 16  # whole frames: resident rows 0..H (ya0 = 0)
+    plane = rows * ((w + 15) & ~15)
+    r256 = lambda v: (v + 255) & ~255  # noqa: E731
+    stride = r256(r256(plane) + (2 if h % 16 else 1) * 4 * plane)
+    m = min(MAX_JOBS, (1 << 30) // stride)
+    return min(F, m) if m >= 2 else 1
+
+
 def load_traffic(tag):
     """(HBM bytes per launch of the dominant kernel, per search over all its
     kernels) from the committed rocprofv3 PMC summary of this workload
@@ -655,12 +675,13 @@ def main():
     # Stripe mode: the frame's work / N against the slowest rank's kernel time.
     # Priced per launch of the dominant kernel.  SAD batches share launches of
     # up to MAX_JOBS (32) frames (1080p: the flow kernel's job table; 4K / 8K:
-    # the item kernel's); SSD launches per frame (prepass + matrix-core kernel).
+    # the item kernel's); B = 16 SSD batches share a prepass and a block-major
+    # launch (ssd_frames_per_launch), 8x8 SSD launches per frame.
     # So a launch holds fpl frames and lasts kern_ms * fpl / F.  Stripe mode:
     # the rank's F stripes, one launch per step (F <= 32).  roofline.traffic is
     # the PMC bytes per launch of the same workload at the same F
     # (tools/profile_all.sh -> profiles/pmc_summary.json).
-    fpl = min(F, MAX_JOBS) if args.cost == "sad" else 1
+    fpl = min(F, MAX_JOBS) if args.cost == "sad" else ssd_frames_per_launch(w, h, blk, span, F)
     if mode == "frames":
         alg_bytes = fpl * (2 * w * h + 8 * nb)
         launch_ms = kern_ms * fpl / F
@@ -737,7 +758,7 @@ def main():
                                             cands_frame, dev, min(args.steps * F, 100))
     if (rank == 0 and world == 1 and mode == "frames" and args.cost == "sad"
             and blk == 16 and not args.no_ssd):
-        line["ssd_mfma"] = ssd_beside(eng, ref_t[0], cur_t[0], blk, span, nb, cands_frame, dev,
+        line["ssd_mfma"] = ssd_beside(eng, ref_t, cur_t, blk, span, nb, cands_frame, dev,
                                       min(args.steps, 20))
     if parity is not None:
         line["stripe_gather_parity"] = parity

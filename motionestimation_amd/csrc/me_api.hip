@@ -67,6 +67,7 @@ static Tuning read_tuning() {
   env_int("ME_STRIP", 0, 64, &t.strip);
   env_int("ME_FAIR", 0, 3, &t.fair);
   env_int("ME_FLOW_ONE", 0, 1, &t.flow_one);
+  env_int("ME_MFMA_BATCH", 0, 1, &t.mfma_batch);
   if (const char* e = getenv("ME_FAIR_T")) {
     int lo = 0, hi = 0;
     if (sscanf(e, "%d,%d", &lo, &hi) == 2 && lo >= 1 && lo <= hi && hi <= 255) {
@@ -180,7 +181,7 @@ SearchArgs make_args(const uint8_t* ref, int ref_row0, const uint8_t* cur, int c
   return p;
 }
 
-me_status attach_scratch(me_ctx* c, Dev& d, SearchArgs& p, bool cap) {
+me_status attach_scratch(me_ctx* c, Dev& d, SearchArgs& p, bool cap, int batch) {
   p.sched = d.sched;
   {
     const size_t tiles = merge_tiles_needed(p);
@@ -202,7 +203,8 @@ me_status attach_scratch(me_ctx* c, Dev& d, SearchArgs& p, bool cap) {
   p.mkeys = d.mkeys;
   p.mcnt = d.mcnt;
   p.merge_tiles = d.merge_cap;
-  const size_t need = mfma_ssd_scratch(p);
+  // a batch of equal jobs: prepass planes for a launch's worth of them
+  const size_t need = batch > 1 ? mfma_batch_scratch(p, batch) : mfma_ssd_scratch(p);
   if (need && cap && (need > d.scratch_cap || !d.scratch))
     return fail(c, ME_EINVAL, "captured search needs new scratch: run it once uncaptured first");
   if (need) {
@@ -696,7 +698,13 @@ me_status me_search_stripes_device(me_ctx* c, int width, int height, int stride,
                    stride, blk, range, cost, jobs[0].block_row_begin, jobs[0].block_row_end,
                    jobs[0].d_mv_xy, jobs[0].d_block_cost);
   {
-    me_status s = attach_scratch(c, d, base, cap);
+    // jobs of one geometry (a batch of whole frames) share the SSD launches
+    bool same = true;
+    for (int i = 1; i < n_jobs; i++)
+      same = same && jobs[i].block_row_begin == jobs[0].block_row_begin &&
+             jobs[i].block_row_end == jobs[0].block_row_end && jobs[i].ref_row0 == jobs[0].ref_row0 &&
+             jobs[i].cur_row0 == jobs[0].cur_row0;
+    me_status s = attach_scratch(c, d, base, cap, same ? n_jobs : 1);
     if (s != ME_OK) return s;
   }
   c->err[0] = 0;

@@ -73,7 +73,9 @@ SearchArgs make_args(const uint8_t* ref, int ref_row0, const uint8_t* cur, int c
 // with launch_ordered.
 // cap: the launch is being captured (me_capture_begin): growing the scratch
 // then fails with ME_EINVAL (a graph must not hold buffers a later search frees).
-me_status attach_scratch(me_ctx* c, Dev& d, SearchArgs& p, bool cap = false);
+// batch > 1: scratch for that many equal-geometry jobs in shared launches
+// (mfma_batch_scratch), else for one search
+me_status attach_scratch(me_ctx* c, Dev& d, SearchArgs& p, bool cap = false, int batch = 1);
 
 // Launch p (scratch attached) on stream s after every earlier search of d:
 // a search arriving on a different stream than the previous one first waits

@@ -103,6 +103,20 @@ struct FlowJobs {
   uint32_t* cost[MAX_JOBS];
 };
 
+// Equal-geometry SSD searches of one matrix-core launch pair (prepass + main
+// kernel): frames of one size and the same block rows.  Job j's planes and
+// records are its own, its prepass planes sit at scratch + j * scratch_stride.
+// A single search is the one-job table of its own pointers.
+struct MfmaJobs {
+  int n;
+  int wgs;                // main-kernel workgroups per job
+  size_t scratch_stride;  // bytes between consecutive jobs' prepass planes
+  const uint8_t* ref[MAX_JOBS];
+  const uint8_t* cur[MAX_JOBS];
+  int16_t* mv[MAX_JOBS];
+  uint32_t* cost[MAX_JOBS];
+};
+
 // Search every job (geometry, cost and scratch from base): SAD jobs the flow
 // kernel takes share one launch (up to MAX_JOBS jobs), VALU jobs of the item
 // kernel likewise, everything else runs job by job through launch_search.
@@ -136,6 +150,14 @@ size_t mfma_merge_tiles(const SearchArgs& p);  // tiles the merge buffers must c
 bool plan_mfma_ssd(const SearchArgs& p, MfmaGeom* g);
 hipError_t launch_mfma_ssd(const SearchArgs& p, const MfmaGeom& g, hipStream_t stream);
 size_t mfma_ssd_scratch(const SearchArgs& p);  // 0: path not applicable
+// Scratch for n equal-geometry jobs of p's shape in batched launches (the
+// block-major kernel; at most MAX_JOBS per launch, capped near 1 GiB), or
+// mfma_ssd_scratch(p) when they would run one by one.
+size_t mfma_batch_scratch(const SearchArgs& p, int n);
+// Equal-geometry SSD jobs on the block-major kernel, in launches of as many
+// jobs as the scratch holds.  False (nothing launched): not applicable.
+bool launch_mfma_jobs(const SearchArgs& base, const SearchJob* jobs, int n, hipStream_t stream,
+                      hipError_t* err);
 // Tiles of cross-workgroup merge buffers (mkeys: 16 u64 keys each, ~0; mcnt:
 // one u32 counter each, 0) the search of p needs (the MFMA SSD kernels).
 size_t merge_tiles_needed(const SearchArgs& p);

@@ -1930,7 +1930,9 @@ static hipError_t launch_valu(const SearchArgs& p, hipStream_t stream, int* used
 hipError_t launch_jobs(const SearchArgs& base, const SearchJob* jobs, int n, hipStream_t stream) {
   hipError_t e;
   if (n > 1 && launch_flow_jobs(base, jobs, n, stream, &e)) return e;
-  // SSD jobs the matrix cores take go one by one (their prepass planes are per search)
+  // SSD jobs of one geometry share the matrix cores' launches (prepass planes
+  // per job in the context scratch); others go one by one
+  if (n > 1 && launch_mfma_jobs(base, jobs, n, stream, &e)) return e;
   MfmaGeom mg;
   const bool mfma = base.cost_kind == COST_SSD && base.scratch && plan_mfma_ssd(job_args(base, jobs[0]), &mg);
   if (n > 1 && !mfma && launch_item_jobs(base, jobs, n, stream, &e)) return e;

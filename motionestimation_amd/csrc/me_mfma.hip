@@ -103,6 +103,18 @@ __device__ __forceinline__ int opaque(int v) {
   return v;
 }
 
+// Job j of a batched launch: its planes, records and prepass planes.
+__device__ __forceinline__ void mfma_job(const MfmaJobs& jb, int j, SearchArgs& p, MfmaGeom& g) {
+  p.ref = jb.ref[j];
+  p.cur = jb.cur[j];
+  p.mv = jb.mv[j];
+  p.cost = jb.cost[j];
+  const size_t off = (size_t)j * jb.scratch_stride;
+  g.rp += off;
+  g.s2 = reinterpret_cast<int*>(reinterpret_cast<uint8_t*>(g.s2) + off);
+  if (g.s2h) g.s2h = reinterpret_cast<int*>(reinterpret_cast<uint8_t*>(g.s2h) + off);
+}
+
 // -------------------------------------------------------------- prepass
 // Plane row rr is frame row ya0 + rr; every plane holds rows_alloc rows of
 // `pitch` entries, all written (the main kernel's masked candidates read the
@@ -210,7 +222,8 @@ __device__ __forceinline__ void prep_tile(const SearchArgs& p, const MfmaGeom& g
 }
 
 template <int B>
-__global__ __launch_bounds__(PREP_T) void me_ssd_prep_kernel(SearchArgs p, MfmaGeom g) {
+__global__ __launch_bounds__(PREP_T) void me_ssd_prep_kernel(SearchArgs p, MfmaGeom g, MfmaJobs jb) {
+  mfma_job(jb, (int)blockIdx.z, p, g);  // z: the job of a batched launch
   __shared__ __align__(16) int vs[64 * VS_P];
   __shared__ __align__(16) uint8_t rpt[64 * RPT_P];
   // blockIdx.y < nmain: rp and s2 rows [64 y, +64); past it: s2h rows from s2h_row0
@@ -913,7 +926,7 @@ constexpr int BM_HDR = 8 * 16 * BM_CREC + 8 * 8 + 8 * 4;  // records, keys, cc
 
 template <int LP>
 __global__ __launch_bounds__(256)
-__attribute__((amdgpu_waves_per_eu(4))) void me_mfma_bm16_kernel(SearchArgs p, MfmaGeom g) {
+__attribute__((amdgpu_waves_per_eu(4))) void me_mfma_bm16_kernel(SearchArgs p, MfmaGeom g, MfmaJobs jb) {
   constexpr int BM_LP = LP;
   constexpr int BM_WINB = 31 * LP;  // one band's window rows
   extern __shared__ __align__(16) uint8_t smem[];
@@ -931,6 +944,11 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_bm16_kernel(SearchArgs p, M
     const int nwg = (int)gridDim.x, bid = (int)blockIdx.x;
     const int x = bid & 7, m = bid >> 3, q = nwg >> 3, rem = nwg & 7;
     lin = x * q + min(x, rem) + m;
+  }
+  {  // batched launch: jobs are consecutive runs of jb.wgs workgroups
+    const int j = lin / jb.wgs;
+    lin -= j * jb.wgs;
+    mfma_job(jb, j, p, g);
   }
   const int brl = lin / g.bm_wpr, sx = lin - brl * g.bm_wpr;
   const int br = g.row0 + brl;
@@ -1378,15 +1396,45 @@ static bool plan_mfma_ssd8(const SearchArgs& p, MfmaGeom* g) {
   return true;
 }
 
-hipError_t launch_mfma_ssd(const SearchArgs& p, const MfmaGeom& g, hipStream_t stream) {
+// The one-job table of a single search (its own pointers, its own scratch).
+static MfmaJobs single_job(const SearchArgs& p, const MfmaGeom& g) {
+  MfmaJobs jb;
+  jb.n = 1;
+  jb.wgs = g.nrows * g.bm_wpr;
+  jb.scratch_stride = 0;
+  jb.ref[0] = p.ref;
+  jb.cur[0] = p.cur;
+  jb.mv[0] = p.mv;
+  jb.cost[0] = p.cost;
+  return jb;
+}
+
+// Prepass over every job of the table (grid z = job).
+static hipError_t launch_prep(const SearchArgs& p, const MfmaGeom& g, const MfmaJobs& jb,
+                              hipStream_t stream) {
   const int nmain = (g.rows_alloc + 63) / 64;
   const int nh = g.hb_row >= 0 ? (g.rows_alloc - g.s2h_row0 + 63) / 64 : 0;
-  dim3 pgrid((unsigned)((g.pitch + 63) / 64), (unsigned)(nmain + nh));
+  dim3 pgrid((unsigned)((g.pitch + 63) / 64), (unsigned)(nmain + nh), (unsigned)jb.n);
   if (p.blk == 8)
-    hipLaunchKernelGGL(me_ssd_prep_kernel<8>, pgrid, dim3(PREP_T), 0, stream, p, g);
+    hipLaunchKernelGGL(me_ssd_prep_kernel<8>, pgrid, dim3(PREP_T), 0, stream, p, g, jb);
   else
-    hipLaunchKernelGGL(me_ssd_prep_kernel<16>, pgrid, dim3(PREP_T), 0, stream, p, g);
-  hipError_t e = hipGetLastError();
+    hipLaunchKernelGGL(me_ssd_prep_kernel<16>, pgrid, dim3(PREP_T), 0, stream, p, g, jb);
+  return hipGetLastError();
+}
+
+static hipError_t launch_bm16(const SearchArgs& p, const MfmaGeom& g, const MfmaJobs& jb,
+                              hipStream_t stream) {
+  const dim3 gridb((unsigned)(jb.n * jb.wgs));
+  if (g.bm_lp == 288)
+    hipLaunchKernelGGL(me_mfma_bm16_kernel<288>, gridb, dim3(256), g.lds, stream, p, g, jb);
+  else
+    hipLaunchKernelGGL(me_mfma_bm16_kernel<544>, gridb, dim3(256), g.lds, stream, p, g, jb);
+  return hipGetLastError();
+}
+
+hipError_t launch_mfma_ssd(const SearchArgs& p, const MfmaGeom& g, hipStream_t stream) {
+  const MfmaJobs jb = single_job(p, g);
+  hipError_t e = launch_prep(p, g, jb, stream);
   if (e != hipSuccess) return e;
   if (p.blk == 8) {
     const dim3 grid8((unsigned)(g.tiles_x * g.tiles_y));
@@ -1395,14 +1443,7 @@ hipError_t launch_mfma_ssd(const SearchArgs& p, const MfmaGeom& g, hipStream_t s
     hipLaunchKernelGGL(me_mfma_ssd8_kernel<ME_SSD8_KM>, grid8, dim3(256), g.lds, stream, p, g);
     return hipGetLastError();
   }
-  if (g.bm) {
-    const dim3 gridb((unsigned)(g.nrows * g.bm_wpr));
-    if (g.bm_lp == 288)
-      hipLaunchKernelGGL(me_mfma_bm16_kernel<288>, gridb, dim3(256), g.lds, stream, p, g);
-    else
-      hipLaunchKernelGGL(me_mfma_bm16_kernel<544>, gridb, dim3(256), g.lds, stream, p, g);
-    return hipGetLastError();
-  }
+  if (g.bm) return launch_bm16(p, g, jb, stream);
   const int wpt = (g.ngx + g.ngxw - 1) / g.ngxw;
   const dim3 grid((unsigned)(g.tiles_x * g.tiles_y * wpt));
 #define ME_MFMA_CASE(NG, KK)                                                              \
@@ -1415,6 +1456,71 @@ hipError_t launch_mfma_ssd(const SearchArgs& p, const MfmaGeom& g, hipStream_t s
   ME_MFMA_CASE(1, 2) ME_MFMA_CASE(1, 3) ME_MFMA_CASE(2, 2) ME_MFMA_CASE(2, 3)
 #undef ME_MFMA_CASE
   return hipErrorInvalidValue;
+}
+
+// ------------------------------------------------------------------ batches
+// A batch of frames with one geometry shares one prepass launch and one
+// block-major launch: a 1080p search is one round of workgroups per CU, so a
+// launch per frame pays the grid's fill and drain every frame.
+static constexpr size_t MFMA_BATCH_SCRATCH = (size_t)1 << 30;  // prepass planes per launch
+
+static size_t batch_stride(const MfmaGeom& g) { return (g.scratch_bytes + 255) & ~(size_t)255; }
+
+// Jobs per batched launch for this geometry: 0 when the batch path does not
+// apply (not the block-major kernel, or one job's planes alone exceed the cap).
+static int batch_jobs(const MfmaGeom& g, int n) {
+  if (!g.bm || n < 2) return 0;
+  const size_t per = MFMA_BATCH_SCRATCH / batch_stride(g);
+  const int m = (int)(per < (size_t)MAX_JOBS ? per : (size_t)MAX_JOBS);
+  return m >= 2 ? (n < m ? n : m) : 0;
+}
+
+size_t mfma_batch_scratch(const SearchArgs& p, int n) {
+  MfmaGeom g;
+  if (!plan_mfma_ssd(p, &g)) return 0;
+  const int m = batch_jobs(g, n);
+  return m ? (size_t)m * batch_stride(g) : g.scratch_bytes;
+}
+
+bool launch_mfma_jobs(const SearchArgs& base, const SearchJob* jobs, int n, hipStream_t stream,
+                      hipError_t* err) {
+  *err = hipSuccess;
+  if (base.cost_kind != COST_SSD || n < 2 || !base.scratch || tuning().mfma_batch == 0) return false;
+  for (int i = 1; i < n; i++)  // one geometry: the same rows of same-sized frames
+    if (jobs[i].r0 != jobs[0].r0 || jobs[i].r1 != jobs[0].r1 ||
+        jobs[i].ref_row0 != jobs[0].ref_row0 || jobs[i].cur_row0 != jobs[0].cur_row0)
+      return false;
+  SearchArgs p = base;
+  p.ref = jobs[0].ref;
+  p.ref_row0 = jobs[0].ref_row0;
+  p.cur = jobs[0].cur;
+  p.cur_row0 = jobs[0].cur_row0;
+  p.block_row_begin = jobs[0].r0;
+  p.block_row_end = jobs[0].r1;
+  p.mv = jobs[0].mv;
+  p.cost = jobs[0].cost;
+  MfmaGeom g;
+  if (jobs[0].r1 <= jobs[0].r0 || !plan_mfma_ssd(p, &g)) return false;
+  const size_t stride = batch_stride(g);
+  int m = batch_jobs(g, n);
+  if (m && (size_t)m * stride > base.scratch_bytes) m = (int)(base.scratch_bytes / stride);
+  if (m < 2 || g.nbx < p.nbx) return false;  // (a partial right column: job by job)
+  for (int i0 = 0; i0 < n && *err == hipSuccess; i0 += m) {
+    MfmaJobs jb;
+    jb.n = n - i0 < m ? n - i0 : m;
+    jb.wgs = g.nrows * g.bm_wpr;
+    jb.scratch_stride = stride;
+    for (int j = 0; j < jb.n; j++) {
+      const SearchJob& J = jobs[i0 + j];
+      jb.ref[j] = J.ref;
+      jb.cur[j] = J.cur;
+      jb.mv[j] = J.mv;
+      jb.cost[j] = J.cost;
+    }
+    *err = launch_prep(p, g, jb, stream);
+    if (*err == hipSuccess) *err = launch_bm16(p, g, jb, stream);
+  }
+  return true;
 }
 
 }  // namespace me

@@ -27,6 +27,7 @@ struct Tuning {
                           // with refills (automatic), 2 on items whose slot gets a refill, 3 always
   int fair_lo = 8, fair_hi = 16;  // ME_FAIR_T=lo,hi: the lags (pulls) that raise a wave to priority 1 / 2
   int flow_one = -1;      // ME_FLOW_ONE=0|1: a batch's flow jobs in launches of one ring / in one launch (-1 = automatic: one)
+  int mfma_batch = -1;    // ME_MFMA_BATCH=0|1: equal SSD jobs share matrix-core launches (-1 = automatic: on)
   int strip = -1;         // ME_STRIP=0..64: item-kernel tile strips (0 = row-major; -1 = automatic)
 };
 
