@@ -420,6 +420,33 @@ def test_batch_search_equals_per_frame(engine, cost, blk, span, w, h, ways):
     engine.device_check()
 
 
+@pytest.mark.parametrize("cost", ["ssd", "sad"])
+def test_batch_past_one_launch(engine, cost):
+    """A batch longer than one launch's job table (MAX_JOBS = 32): 40 frames
+    of a frame with a partial bottom block row run as 32 + 8 jobs (SSD: shared
+    prepass + block-major launches; SAD: the flow kernel's job table) and equal
+    the oracle frame by frame."""
+    import torch
+    F, w, h, blk, span = 40, 160, 120, 16, 32
+    base_ref, base_cur = synth.frame_pair(w, h, 7, -2, 5)
+    frames = [(np.roll(base_ref, 11 * f, axis=1), np.roll(base_cur, 11 * f, axis=1))
+              for f in range(F)]
+    ref_b = torch.from_numpy(np.stack([r for r, _ in frames])).cuda()
+    cur_b = torch.from_numpy(np.stack([c for _, c in frames])).cuda()
+    nb = me.num_blocks(w, h, blk)
+    mv = torch.full((F * nb, 2), -5, dtype=torch.int16, device="cuda")
+    co = torch.zeros(F * nb, dtype=torch.int32, device="cuda")
+    engine.search_batch_device(ref_b, 0, cur_b, 0, w, h, blk, span, cost, 0, (h + blk - 1) // blk,
+                               mv, co)
+    torch.cuda.synchronize()
+    mv, co = mv.cpu().numpy(), co.cpu().numpy().view(np.uint32)
+    for f, (r, c) in enumerate(frames):
+        omv, oco, _ = O.full_search(r, c, blk, span, cost, threads=NT)
+        np.testing.assert_array_equal(mv[f * nb:(f + 1) * nb], omv, err_msg=f"{cost} frame {f}")
+        np.testing.assert_array_equal(co[f * nb:(f + 1) * nb], oco, err_msg=f"{cost} frame {f}")
+    engine.device_check()
+
+
 def test_batch_search_argument_checks(engine):
     import torch
     L = me._lib.lib()
