@@ -44,14 +44,14 @@ static Tuning read_tuning() {
   if (const char* e = getenv("ME_PLAN")) {
     int v[5] = {0, 0, 0, 0, -1};
     const int n = sscanf(e, "%d,%d,%d,%d,%d", &v[0], &v[1], &v[2], &v[3], &v[4]);
-    const bool ok = n >= 4 && (v[0] == 0 || v[0] == 4 || v[0] == 5 || v[0] == 8 || v[0] == 11 || v[0] == 13) &&
+    const bool ok = n >= 4 && (v[0] == 0 || v[0] == 4 || v[0] == 5 || v[0] == 8 || v[0] == 11 || v[0] == 13 || v[0] == 26) &&
                     v[1] >= 0 && v[1] <= 16 && v[2] >= 0 && v[2] <= 64 &&
                     (v[3] == 0 || (v[3] >= 64 && v[3] <= 1024 && v[3] % 64 == 0)) &&
                     v[4] >= -1 && v[4] <= 1;
     if (ok) {
       t.plan_k = v[0]; t.plan_tb = v[1]; t.plan_cpp = v[2]; t.plan_threads = v[3]; t.plan_fold = v[4];
     } else {
-      fprintf(stderr, "me_hip: ignoring ME_PLAN=%s (K in {0,4,5,8,11,13}, tb 0..16, cpp 0..64, "
+      fprintf(stderr, "me_hip: ignoring ME_PLAN=%s (K in {0,4,5,8,11,13,26}, tb 0..16, cpp 0..64, "
                       "threads 0 or 64..1024 step 64, fold -1..1)\n", e);
     }
   }

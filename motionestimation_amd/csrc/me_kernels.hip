@@ -299,29 +299,45 @@ __device__ unsigned long long g_wstamps[8 << 14];
 // no literals: larger ones would each pin a VGPR and spill); invalid
 // candidates forced to sad 0xFFFF (> any valid SAD: B*B*255 <= 65280).
 // MASKJ = false on items whose whole dy range is valid (uniform per item).
-template <int K, bool MASKJ>
-__device__ __forceinline__ uint32_t lane_best(const uint64_t (&acc)[K], uint32_t mlo,
-                                              uint32_t mhi, int jlo, int jhi) {
+template <int K, int J0, int J1, bool MASKJ>
+__device__ __forceinline__ uint32_t lane_best_rows(const uint64_t (&acc)[K], uint32_t mlo,
+                                                   uint32_t mhi, int jlo, int jhi) {
   // Two independent min3 chains (i = 0,1 and i = 2,3): the epilogues of all
   // waves on a SIMD tend to coincide (item barriers), so a single 2K-deep
   // dependent chain would run at VALU latency, not issue rate.
   uint32_t b01 = ~0u, b23 = ~0u;
 #pragma unroll
-  for (int j = 0; j < K; j++) {
+  for (int j = J0; j < J1; j++) {
     uint32_t lo = (uint32_t)acc[j] | mlo, hi = (uint32_t)(acc[j] >> 32) | mhi;
     if (MASKJ) {
       const bool jv = j >= jlo && j <= jhi;
       lo = jv ? lo : ~0u;
       hi = jv ? hi : ~0u;
     }
-    const uint32_t k0 = (lo << 16) | (uint32_t)(5 * j);
-    const uint32_t k1 = (lo & 0xFFFF0000u) | (uint32_t)(5 * j + 1);
-    const uint32_t k2 = (hi << 16) | (uint32_t)(5 * j + 2);
-    const uint32_t k3 = (hi & 0xFFFF0000u) | (uint32_t)(5 * j + 3);
+    const uint32_t k0 = (lo << 16) | (uint32_t)(5 * (j - J0));
+    const uint32_t k1 = (lo & 0xFFFF0000u) | (uint32_t)(5 * (j - J0) + 1);
+    const uint32_t k2 = (hi << 16) | (uint32_t)(5 * (j - J0) + 2);
+    const uint32_t k3 = (hi & 0xFFFF0000u) | (uint32_t)(5 * (j - J0) + 3);
     b01 = min(b01, min(k0, k1));
     b23 = min(b23, min(k2, k3));
   }
   return min(b01, b23);
+}
+
+// K > 13 (26: 8x8 SAD): two runs of 13 rows, each with inline-constant
+// indices; the second's keys move past the first's (+ 5 * 13), so the min
+// still orders by (sad, j, i).  A lane key's index is 5 j + i for every K.
+template <int K, bool MASKJ>
+__device__ __forceinline__ uint32_t lane_best(const uint64_t (&acc)[K], uint32_t mlo,
+                                              uint32_t mhi, int jlo, int jhi) {
+  if constexpr (K <= 13) {
+    return lane_best_rows<K, 0, K, MASKJ>(acc, mlo, mhi, jlo, jhi);
+  } else {
+    const uint32_t a = lane_best_rows<K, 0, 13, MASKJ>(acc, mlo, mhi, jlo, jhi);
+    uint32_t b = lane_best_rows<K, 13, K, MASKJ>(acc, mlo, mhi, jlo, jhi);
+    b = b < 0xFFFF0000u ? b + 65u : b;  // (an all-masked run stays ~0)
+    return min(a, b);
+  }
 }
 
 // Fold column: SAD of the lane's one dx = +S candidate (window rows row..row+H-1,
@@ -1244,7 +1260,12 @@ bool plan_fast(const SearchArgs& p, QsadGeom* g, int* k_out) {
   // of 144 bytes; the 2- and 4-way stripe times moved within box-to-box
   // noise, profiles/r02al_stripe_sweeps.jsonl)
   const int aw = S % 4 == 0 ? 0 : 4;
-  static const int Ks[] = {13, 11, 8, 5};
+  static const int Ks[] = {26, 13, 11, 8, 5};
+  // K = 26 (8x8 SAD): twice the candidates per lane-task, so the task decode,
+  // cur loads, fold column and key merge are paid per 104 candidates, not 52
+  // (8K +-128: 18.23 -> 17.40 ms, tb 8 at the compiled pitch 336;
+  // profiles/r03ar_plan_8k.jsonl)
+  const bool k26_auto = sad && B == 8;
   // K = 5 (a quarter-size wave-task) only for SAD searches too small to give
   // every SIMD two K = 13 wave-tasks (an 8-way 1080p stripe: 1.25 per SIMD, so
   // a quarter of the SIMDs ran a second round); K >= 8 otherwise.
@@ -1273,8 +1294,10 @@ bool plan_fast(const SearchArgs& p, QsadGeom* g, int* k_out) {
     const double use_dx = sad ? (fold ? 1.0 : (double)D / (4.0 * G)) : 1.0;
     for (int K : Ks) {
       if (force[0] && K != force[0]) continue;
-      // (K = 5 is instantiated for 16x16 SAD only: other small searches keep K >= 8)
+      // (K = 5 is instantiated for 16x16 SAD only: other small searches keep K >= 8;
+      // K = 26 for 8x8 SAD only)
       if (K == 5 && (!sad || B != 16)) continue;
+      if (K == 26 && (!sad || B != 8 || (!force[0] && !k26_auto))) continue;
       if (!force[0] && (K == 5) != (small && B == 16)) continue;
       if (fold && G < K) continue;
       const int chunks = (D + K - 1) / K;
@@ -1343,7 +1366,10 @@ bool plan_fast(const SearchArgs& p, QsadGeom* g, int* k_out) {
           const double fill = tiles >= 2048 ? 1.0 : (double)tiles / 2048;
           // K = 13 measured best wherever it fits (more candidates per row load
           // and per epilogue than the padding it costs).
-          const double kpref = K == 13 ? 1.0 : 0.95;
+          // K = 26 over K = 13 where it fits (8x8 SAD), at the compiled tile
+          // pitch 336 if a tb gives it (tb 8: 17.40 ms; tb 12 / 16 at runtime
+          // pitches 17.68 / 17.64 ms)
+          const double kpref = K == 26 ? (pt == 336 ? 1.05 : 1.03) : K == 13 ? 1.0 : 0.95;
           // the last tile of a block row holds nbx_full % tb blocks
           const double tile_fill =
               (double)g->nbx_full / ((double)((g->nbx_full + tb - 1) / tb) * tb);
@@ -1629,6 +1655,7 @@ static hipError_t launch_fast(const SearchArgs& p, QsadGeom g, int K, const Flow
   ME_FAST_CASE(COST_SAD, 16, 13) ME_FAST_CASE(COST_SAD, 16, 11) ME_FAST_CASE(COST_SAD, 16, 8)
   ME_FAST_CASE(COST_SAD, 16, 5)
   ME_FAST_CASE(COST_SAD, 8, 13) ME_FAST_CASE(COST_SAD, 8, 11) ME_FAST_CASE(COST_SAD, 8, 8)
+  ME_FAST_CASE_P(COST_SAD, 8, 26, 336) ME_FAST_CASE(COST_SAD, 8, 26)
   ME_FAST_CASE(COST_SSD, 16, 13) ME_FAST_CASE(COST_SSD, 16, 11) ME_FAST_CASE(COST_SSD, 16, 8)
   ME_FAST_CASE(COST_SSD, 8, 13) ME_FAST_CASE(COST_SSD, 8, 11) ME_FAST_CASE(COST_SSD, 8, 8)
 #undef ME_FAST_CASE
