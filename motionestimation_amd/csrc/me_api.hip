@@ -328,8 +328,8 @@ me_status stripe_upload_launch(me_ctx* c, Dev& d, const uint8_t* ref, const uint
   return launch_ordered(c, d, p, d.stream);
 }
 
-// Multi-device frame search: row stripes balanced by candidate count, one per
-// context device.  One host thread per device uploads its stripe
+// Multi-device frame search: row stripes balanced by me_plan_stripes' per-row
+// cost model (include/me.h), one per context device.  One host thread per device uploads its stripe
 // (pageable host planes are staged by the runtime, so the uploads of the
 // devices overlap instead of running one after another) and enqueues its
 // search; then one ncclGather of the padded per-stripe records to device 0.

@@ -261,6 +261,9 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, uint8_t* lds_ds
   }
 }
 
+#ifndef ME_ABL
+#define ME_ABL 0  // diagnostic ablations of the block-major kernel (never in libme_hip.so)
+#endif
 #define MFMA16 __builtin_amdgcn_mfma_i32_16x16x64_i8
 
 __device__ __forceinline__ uint32_t sad_u32(uint32_t a_sgpr, uint32_t b, uint32_t c) {
@@ -1107,8 +1110,12 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_bm16_kernel(SearchArgs p, M
       auto tile = [&](int i, auto DA, auto DB, auto MA, auto MB) {
         constexpr bool da = decltype(DA)::value, db = decltype(DB)::value;
         constexpr int ma = decltype(MA)::value, mb = decltype(MB)::value;
+#if ME_ABL == 1  // diagnostic build: no S2 loads (timing only, keys wrong)
+        const v4i s2c = {srow, s2v, i, 0};
+#else
         const v4i s2c = __builtin_bit_cast(
             v4i, __builtin_amdgcn_raw_buffer_load_b128(rs2, s2v, srow + 64 * i, 0));
+#endif
         // one base per tile, fragment rows at immediate offsets
         const uint32_t lrow = (uint32_t)opaque((int)(lrow0 + (uint32_t)(16 * i)));
         v4i accA = ma == 1 ? mF : ma == 2 ? mL : zero4;
@@ -1116,6 +1123,9 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_bm16_kernel(SearchArgs p, M
         // Fragments in pairs, the next pair in flight during this pair's MFMAs
         // (four fragments live: the A fragments hold 64 VGPRs).
         auto ld = [&](int q) {
+#if ME_ABL == 3  // diagnostic build: two fragment rows per tile (a quarter of the LDS reads)
+          q &= 1;
+#endif
           return *reinterpret_cast<lds_v4i*>((uintptr_t)(lrow + (uint32_t)(2 * q * BM_LP)));
         };
         v4i f0 = ld(0), f1 = ld(1);
@@ -1142,6 +1152,11 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_bm16_kernel(SearchArgs p, M
 #pragma unroll
         for (int r = 0; r < 4; r++) P[r] = lshl6_add((uint32_t)s2c[r], kb + (uint32_t)r);
         auto keys_of = [&](v4i acc, uint32_t& best, int i0, int i1, int e0, auto GEN) {
+#if ME_ABL == 2  // diagnostic build: no key epilogue (timing only)
+          asm volatile("" : : "v"(acc), "v"(P[0]));
+          best ^= (uint32_t)acc[0];
+          return;
+#endif
           if constexpr (decltype(GEN)::value) {
             if (i == i0 || i == i1) {
               const int e = i == i0 ? e0 : e0 + 1;
