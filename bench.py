@@ -519,6 +519,14 @@ def stripe_record(eng, dev, world, rank, gloo, cfg_name, cost, steps, warmup, nf
             "gather": sr.gather_impl()}
 
 
+def sad_frames_per_launch(w, h, blk, span, F):
+    """Frames per SAD launch of an F-frame batch: one launch of up to MAX_JOBS
+    frames, except frames of >= 2^33 window positions (blocks x (2S+1)^2: 8K
+    8x8 +-128), which launch one by one (me_kernels.hip launch_item_jobs)."""
+    nb = ((w + blk - 1) // blk) * ((h + blk - 1) // blk)
+    return 1 if nb * (2 * span + 1) ** 2 >= 1 << 33 else min(F, MAX_JOBS)
+
+
 def ssd_frames_per_launch(w, h, blk, span, F):
     """Frames per matrix-core launch pair of an F-frame SSD batch (me_mfma.hip
     launch_mfma_jobs): B = 16 (block-major kernel, S <= 192) batches as many
@@ -674,14 +682,15 @@ def main():
     # VALU work: the exact abs-diff count (w*h of each block, not B*B).
     # Stripe mode: the frame's work / N against the slowest rank's kernel time.
     # Priced per launch of the dominant kernel.  SAD batches share launches of
-    # up to MAX_JOBS (32) frames (1080p: the flow kernel's job table; 4K / 8K:
-    # the item kernel's); B = 16 SSD batches share a prepass and a block-major
+    # up to MAX_JOBS (32) frames (1080p: the flow kernel's job table; 4K: the
+    # item kernel's; 8K 8x8 frames launch one by one, sad_frames_per_launch); B = 16 SSD batches share a prepass and a block-major
     # launch (ssd_frames_per_launch), 8x8 SSD launches per frame.
     # So a launch holds fpl frames and lasts kern_ms * fpl / F.  Stripe mode:
     # the rank's F stripes, one launch per step (F <= 32).  roofline.traffic is
     # the PMC bytes per launch of the same workload at the same F
     # (tools/profile_all.sh -> profiles/pmc_summary.json).
-    fpl = min(F, MAX_JOBS) if args.cost == "sad" else ssd_frames_per_launch(w, h, blk, span, F)
+    fpl = (sad_frames_per_launch(w, h, blk, span, F) if args.cost == "sad"
+           else ssd_frames_per_launch(w, h, blk, span, F))
     if mode == "frames":
         alg_bytes = fpl * (2 * w * h + 8 * nb)
         launch_ms = kern_ms * fpl / F

@@ -1922,8 +1922,20 @@ static bool launch_item_jobs(const SearchArgs& base, const SearchJob* jobs, int 
   QsadGeom g;
   int K = 0;
   if (!cached_plan(probe, &g, &K)) return false;
-  for (int i0 = 0; i0 < n && *err == hipSuccess; i0 += MAX_JOBS) {
-    const int m = n - i0 < MAX_JOBS ? n - i0 : MAX_JOBS;
+  // A job that alone fills the chip many times over (blocks x (2S+1)^2 >= 2^33
+  // window positions: 8K 8x8 +-128, 3.4e10, 2.5k items per CU) gains nothing
+  // from sharing a launch (8K: 17.19 vs 17.25 ms per frame) and costs L2
+  // reuse there (124 against 98 MB fetched per frame, profiles/r03aw_*): such
+  // jobs launch one by one (bench.py's item_frames_per_launch mirrors this).
+  const long win = (2L * base.range + 1) * (2L * base.range + 1);
+  long max_pos = 0;
+  for (int i = 0; i < n; i++) {
+    const long pos = (long)base.nbx * (jobs[i].r1 - jobs[i].r0) * win;
+    max_pos = pos > max_pos ? pos : max_pos;
+  }
+  const int per = max_pos >= (1L << 33) ? 1 : MAX_JOBS;
+  for (int i0 = 0; i0 < n && *err == hipSuccess; i0 += per) {
+    const int m = n - i0 < per ? n - i0 : per;
     SearchJob fj[MAX_JOBS];
     for (int i = 0; i < m; i++) {
       fj[i] = jobs[i0 + i];
