@@ -204,7 +204,9 @@ me_status attach_scratch(me_ctx* c, Dev& d, SearchArgs& p, bool cap, int batch) 
   p.mcnt = d.mcnt;
   p.merge_tiles = d.merge_cap;
   // a batch of equal jobs: prepass planes for a launch's worth of them
-  const size_t need = batch > 1 ? mfma_batch_scratch(p, batch) : mfma_ssd_scratch(p);
+  size_t need = batch > 1 ? mfma_batch_scratch(p, batch) : mfma_ssd_scratch(p);
+  const size_t ssim = ssim_scratch(p);  // SSIM jobs run one by one on one plane
+  if (ssim > need) need = ssim;
   if (need && cap && (need > d.scratch_cap || !d.scratch))
     return fail(c, ME_EINVAL, "captured search needs new scratch: run it once uncaptured first");
   if (need) {

@@ -173,6 +173,8 @@ bool plan_fast(const SearchArgs& p, QsadGeom* g, int* k_out);
 
 // SSIM-cost search (me_ssim.hip): every block of rows [block_row_begin, block_row_end).
 hipError_t launch_ssim(const SearchArgs& p, hipStream_t stream);
+// Scratch bytes of the SSIM search's patch-statistics plane (0: not applicable).
+size_t ssim_scratch(const SearchArgs& p);
 
 // Consumers of the MV field (me_post.hip).
 hipError_t launch_compensate(const uint8_t* ref, const uint8_t* cur, int width, int height,

@@ -11,7 +11,9 @@ kernels, and the float replay of SSD for blocks with w*h > 256.
 
 SSD is compared with the oracle's float-MSE mode (the reference's own
 argmin, main.c:18-64): the MV field must equal it and the reported cost is the
-integer SSD of that vector."""
+integer SSD of that vector.  SSIM (the reference's CPU SSIM search,
+src/common/ssim.c:3-108) is compared score bit for score bit on smaller
+random shapes."""
 import os
 
 import numpy as np
@@ -56,3 +58,23 @@ def test_random_configs_against_oracle(engine, seed):
         what = f"seed {seed} case {case}: {w}x{h} B{blk} S{span} {kind} {cost}"
         np.testing.assert_array_equal(mv, omv, err_msg=what)
         np.testing.assert_array_equal(c, oc, err_msg=what)
+
+
+@pytest.mark.parametrize("seed", range(2))
+def test_random_ssim_configs_against_oracle(engine, seed):
+    """The SSIM cost (float replay of src/common/ssim.c) on random shapes:
+    full blocks read the patch-statistics plane, partial ones compute their own;
+    score bits and MVs equal the oracle's."""
+    rng = np.random.default_rng(777 + seed)
+    for case in range(10):
+        blk = int(rng.choice([4, 8, 12, 16, 24]))
+        w = int(rng.integers(max(blk, 24), 161))
+        h = int(rng.integers(max(blk, 24), 121))
+        span = int(rng.integers(0, 25))
+        kind = str(rng.choice(["smooth", "smooth", "noise", "flat", "binary"]))
+        ref, cur = _frames(rng, w, h, kind)
+        mv, bits = engine.full_search(ref, cur, blk, span, "ssim")
+        omv, obits, _ = O.full_search(ref, cur, blk, span, "ssim", threads=NT)
+        what = f"seed {seed} case {case}: {w}x{h} B{blk} S{span} {kind} ssim"
+        np.testing.assert_array_equal(bits, obits, err_msg=what)
+        np.testing.assert_array_equal(mv, omv, err_msg=what)
