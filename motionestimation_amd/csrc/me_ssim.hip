@@ -43,6 +43,7 @@ namespace {
 constexpr int SSIM_THREADS = 256;
 constexpr int SSIM_Q = 4;   // adjacent candidates per lane (in-kernel statistics)
 constexpr int SSIM_QP = 8;  // ... with the statistics plane (one cross chain each)
+constexpr int SSIM_Q16 = 12; // ... 16 x 16 blocks (1080p +-32: 6: 1.27 ms, 8: 0.88, 12: 0.72, 16: 0.81; profiles/r03bc_*, r03bd_*)
 
 __device__ __forceinline__ uint64_t wave_min(uint64_t v) {
 #pragma unroll
@@ -195,6 +196,7 @@ __global__ __launch_bounds__(SSIM_THREADS) void me_ssim_kernel(SearchArgs p, int
                                                                const float2* stats, SsimPlane pg) {
   extern __shared__ __align__(16) uint8_t smem[];
   __shared__ uint64_t red[SSIM_THREADS / 64];
+  __shared__ float ccl[256];  // 16 x 16 blocks with the statistics plane: (c - imc) as floats
   const int tid = threadIdx.x;
   const int bx = (int)(blockIdx.x % (unsigned)p.nbx);
   const int by = row0 + (int)(blockIdx.x / (unsigned)p.nbx);
@@ -249,7 +251,46 @@ __global__ __launch_bounds__(SSIM_THREADS) void me_ssim_kernel(SearchArgs p, int
     return ((uint64_t)(0x7FFFFFFFu - __float_as_uint(score)) << 32) |
            ((uint32_t)(dy + 32768) << 16) | (uint32_t)(dx + 32768);
   };
-  if (stats != nullptr && w == B && h == B) {
+  if (stats != nullptr && B == 16 && w == 16 && h == 16 && staged) {
+    // 16 x 16 blocks, window in LDS: per window row the lane's SSIM_Q16
+    // candidates' 16 + SSIM_Q16 - 1 ref bytes as floats in registers, the
+    // block's (c - imc) as floats in LDS (broadcast reads), the row's 16 pixels
+    // unrolled (no register shifts).  The same chains as below, in the same order.
+    constexpr int Q = SSIM_Q16;
+    for (int i = tid; i < 256; i += SSIM_THREADS) ccl[i] = (float)(cblk[i] - imp);
+    __syncthreads();
+    const int ngq = (ncx + Q - 1) / Q, ng = ngq * ncy;
+    for (int t = tid; t < ng; t += SSIM_THREADS) {
+      const int cy = t / ngq, cx0 = (t - cy * ngq) * Q;
+      const uint8_t* r = win + cy * ww + cx0;  // past the window: the launch's padding
+      const float2* st = stats + (size_t)(wy0 + cy - pg.ylo) * pg.pitch;
+      float fimr[Q], cv[Q];
+#pragma unroll
+      for (int k = 0; k < Q; k++) {
+        fimr[k] = (float)(int)st[min(wx0 + cx0 + k, pg.pitch - 1)].x;
+        cv[k] = 0.f;
+      }
+#pragma unroll 1
+      for (int y = 0; y < 16; y++) {
+        float rf[16 + Q - 1];
+#pragma unroll
+        for (int j = 0; j < 16 + Q - 1; j++) rf[j] = (float)r[y * ww + j];
+#pragma unroll
+        for (int x = 0; x < 16; x++) {
+          const float c = ccl[y * 16 + x];
+#pragma unroll
+          for (int k = 0; k < Q; k++) cv[k] = __fmaf_rn(__fsub_rn(rf[x + k], fimr[k]), c, cv[k]);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < Q; k++) {
+        if (cx0 + k >= ncx) break;
+        const float2 v = st[wx0 + cx0 + k];
+        const uint64_t key = key_of(v.x, v.y, cv[k], cx0 + k, cy);
+        best = key < best ? key : best;
+      }
+    }
+  } else if (stats != nullptr && w == B && h == B) {
     // Full block: patch statistics from the prepass plane; per candidate only
     // the cross chain fl(cv + (r - imr)(c - imc)) in raster order.  The product
     // is an exact integer below 2^24, so fma(r - imr, c - imc, cv) (operands
