@@ -61,6 +61,7 @@ static Tuning read_tuning() {
   env_int("ME_MFMA_NGXW", 1, 2, &t.mfma_ngxw);
   env_int("ME_STREAM_COOL", 1, 64, &t.stream_cool);
   env_int("ME_STREAM_AHEAD", 1, 9, &t.stream_ahead);
+  env_int("ME_STREAM_BATCH", 1, 32, &t.stream_batch);
   env_int("ME_FLOW", 0, 1, &t.flow);
   env_int("ME_FLOW_SLOTS", 2, 16, &t.flow_slots);
   env_int("ME_PRIO", 0, 1, &t.prio);
@@ -249,6 +250,24 @@ me_status launch_ordered(me_ctx* c, Dev& d, SearchArgs& p, hipStream_t s) {
     if (st != ME_OK) return st;
   }
   const hipError_t e = launch_search(p, s, nullptr);
+  if (e != hipSuccess) {
+    if (!cap) {
+      (void)hipMemsetAsync(d.sched, 0, 64, s);
+      if (d.mkeys) (void)hipMemsetAsync(d.mkeys, 0xFF, d.merge_cap * 16 * 8, s);
+      if (d.mcnt) (void)hipMemsetAsync(d.mcnt, 0, d.merge_cap * 4, s);
+    }
+    return fail(c, ME_EDEVICE, "search launch: %s", hipGetErrorString(e));
+  }
+  return ME_OK;
+}
+
+me_status launch_jobs_ordered(me_ctx* c, Dev& d, const SearchArgs& base, const SearchJob* jobs,
+                              int n, hipStream_t s, bool cap) {
+  if (!cap) {
+    me_status st = order_on(c, d, s);
+    if (st != ME_OK) return st;
+  }
+  const hipError_t e = launch_jobs(base, jobs, n, s);
   if (e != hipSuccess) {
     if (!cap) {
       (void)hipMemsetAsync(d.sched, 0, 64, s);
@@ -710,20 +729,7 @@ me_status me_search_stripes_device(me_ctx* c, int width, int height, int stride,
     if (s != ME_OK) return s;
   }
   c->err[0] = 0;
-  if (!cap) {
-    me_status s = me::order_on(c, d, (hipStream_t)stream);
-    if (s != ME_OK) return s;
-  }
-  const hipError_t e = me::launch_jobs(base, js.data(), n_jobs, (hipStream_t)stream);
-  if (e != hipSuccess) {
-    if (!cap) {
-      (void)hipMemsetAsync(d.sched, 0, 64, (hipStream_t)stream);
-      if (d.mkeys) (void)hipMemsetAsync(d.mkeys, 0xFF, d.merge_cap * 16 * 8, (hipStream_t)stream);
-      if (d.mcnt) (void)hipMemsetAsync(d.mcnt, 0, d.merge_cap * 4, (hipStream_t)stream);
-    }
-    return fail(c, ME_EDEVICE, "search launch: %s", hipGetErrorString(e));
-  }
-  return ME_OK;
+  return me::launch_jobs_ordered(c, d, base, js.data(), n_jobs, (hipStream_t)stream, cap);
 }
 
 me_status me_full_search_batch_device(me_ctx* c, const uint8_t* d_ref, size_t ref_frame_stride,

@@ -84,6 +84,12 @@ me_status attach_scratch(me_ctx* c, Dev& d, SearchArgs& p, bool cap = false, int
 // dirty) before returning ME_EDEVICE.
 me_status launch_ordered(me_ctx* c, Dev& d, SearchArgs& p, hipStream_t s);
 
+// The same for a job table (launch_jobs): jobs share base's geometry, cost and
+// scratch (attach_scratch(base, cap, n) for equal jobs).  cap: being captured
+// (no ordering, no state change).
+me_status launch_jobs_ordered(me_ctx* c, Dev& d, const SearchArgs& base, const SearchJob* jobs,
+                              int n, hipStream_t s, bool cap = false);
+
 // Order stream s after the device's previous search (a stream switch) and
 // make s the device's search stream; `launch` then enqueues on s.
 me_status order_on(me_ctx* c, Dev& d, hipStream_t s);

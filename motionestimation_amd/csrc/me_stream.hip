@@ -7,6 +7,10 @@
 // pairs of frames/ForemanYF{1,2,4}) -- and keeps every device busy:
 //   - each frame is uploaded once per device, into a device slot that lives
 //     from the first to the last pair reading it;
+//   - pairs are searched 4 at a time in one job-table launch (launch_jobs),
+//     which pays a launch's fill and drain once per 4 pairs: CIF pan 30.3k ->
+//     38.4k pairs/s; 1080p stays bound by the upload (~22 GB/s H2D), 10.8k ->
+//     11.0k (profiles/r03bn_stream_batch_sweep.txt);
 //   - uploads run on a copy stream, searches on the compute stream; the
 //     host-side staging and upload of pair n+1's new frame overlap the search
 //     of pair n (slots are reused oldest-freed first, so an upload never
@@ -21,6 +25,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <deque>
 #include <map>
 #include <mutex>
@@ -36,6 +41,8 @@ std::mutex g_pin_mu;
 std::map<uintptr_t, size_t> g_pinned;  // me_host_alloc ranges: base -> bytes
 // Freed frame slots kept cooling before reuse (ME_STREAM_COOL overrides; tuning)
 static int cooling_slots() { return tuning().stream_cool > 0 ? tuning().stream_cool : 2; }
+// Pairs per search launch (ME_STREAM_BATCH overrides; tuning)
+constexpr int kPairBatch = 4;
 }  // namespace
 
 bool host_range_pinned(const void* p, size_t bytes) {
@@ -102,6 +109,19 @@ me_status prepare(me_ctx* c, Dev& d, size_t plane) {
     d.slot_bytes = plane;
   }
   if (!d.copy) HIPCHK(c, hipStreamCreateWithFlags(&d.copy, hipStreamNonBlocking));
+  return ME_OK;
+}
+
+// Upload rows [0, H) of a pinned frame (row pitch `stride`) into a slot on the
+// copy stream.  Row chunks on extra streams measured slower (H2D at 1080p: 2
+// streams 10.5k -> 10.5k pairs/s at best and often 4.7k, 3-4 streams 8.9k at
+// best; profiles/r03bm_stream_split_sweep.txt).
+me_status upload_pinned(me_ctx* c, Dev& d, uint8_t* dst, const uint8_t* src, int W, int H,
+                        int stride) {
+  if (stride == W)
+    HIPCHK(c, hipMemcpyAsync(dst, src, (size_t)W * H, hipMemcpyHostToDevice, d.copy));
+  else
+    HIPCHK(c, hipMemcpy2DAsync(dst, W, src, stride, W, H, hipMemcpyHostToDevice, d.copy));
   return ME_OK;
 }
 
@@ -181,66 +201,77 @@ me_status run_pairs(me_ctx* c, Dev& d, const Job& j, int p0, int p1) {
   const int kAhead = env_ahead > 8 ? 1 << 30 : env_ahead >= 1 ? env_ahead : (all_pinned ? 2 : 3);
   for (auto& e : d.pair_ev)
     if (!e) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  for (int n = p0; n < p1; n++) {
-    if (kAhead <= 8 && n - p0 >= kAhead) HIPCHK(c, hipEventSynchronize(d.pair_ev[(n - p0) % kAhead]));
-    for (int side = 0; side < 2; side++) {
-      const int f = j.pairs[2 * n + side];
-      if (slot_of[f] >= 0) continue;
-      // Keep two freed slots cooling: reusing the slot the previous search
-      // just released would serialise this upload behind that search.
-      int si;
-      if (free_slots.size() < (size_t)cooling_slots()) {
-        if ((s = new_slot(c, d, &si)) != ME_OK) return s;
-      } else {
-        si = free_slots.front();
-        free_slots.pop_front();
-        HIPCHK(c, hipStreamWaitEvent(d.copy, d.slot_free[si], 0));
-      }
-      const uint8_t* src = j.frames[f];
-      if (host_range_pinned(src, span)) {
-        if (j.stride == W)
-          HIPCHK(c, hipMemcpyAsync(d.slots[si], src, plane, hipMemcpyHostToDevice, d.copy));
-        else
-          HIPCHK(c, hipMemcpy2DAsync(d.slots[si], W, src, j.stride, W, H, hipMemcpyHostToDevice,
-                                     d.copy));
-      } else {
-        if ((s = ensure_staging(c, d, plane)) != ME_OK) return s;
-        // the copy that last read this staging buffer must be done
-        HIPCHK(c, hipEventSynchronize(d.stage_ev[stage_k]));
-        uint8_t* st = d.stage[stage_k];
-        if (j.stride == W) {
-          memcpy(st, src, plane);
+  // Pairs are searched G at a time in one job-table launch (launch_jobs: the
+  // flow / item kernels' job tables, SSD pairs sharing the matrix cores'
+  // launches), so a launch's fill and drain are paid once per G pairs.  The
+  // slots a batch frees cool while the next batch's frames upload into older
+  // ones: at least G + 1 of them.
+  const int G = tuning().stream_batch > 0 ? tuning().stream_batch : kPairBatch;
+  const size_t cool = (size_t)std::max(cooling_slots(), G + 1);
+  std::vector<SearchJob> jobs;
+  jobs.reserve((size_t)G);
+  int batch = 0;
+  for (int n0 = p0; n0 < p1; n0 += G, batch++) {
+    const int n1 = std::min(p1, n0 + G);
+    if (kAhead <= 8 && batch >= kAhead) HIPCHK(c, hipEventSynchronize(d.pair_ev[batch % kAhead]));
+    jobs.clear();
+    me::SearchArgs base{};
+    for (int n = n0; n < n1; n++) {
+      for (int side = 0; side < 2; side++) {
+        const int f = j.pairs[2 * n + side];
+        if (slot_of[f] >= 0) continue;
+        // Keep freed slots cooling: reusing a slot the previous batch just
+        // released would serialise this upload behind that search.
+        int si;
+        if (free_slots.size() < cool) {
+          if ((s = new_slot(c, d, &si)) != ME_OK) return s;
         } else {
-          for (int y = 0; y < H; y++) memcpy(st + (size_t)y * W, src + (size_t)y * j.stride, W);
+          si = free_slots.front();
+          free_slots.pop_front();
+          HIPCHK(c, hipStreamWaitEvent(d.copy, d.slot_free[si], 0));
         }
-        HIPCHK(c, hipMemcpyAsync(d.slots[si], st, plane, hipMemcpyHostToDevice, d.copy));
-        HIPCHK(c, hipEventRecord(d.stage_ev[stage_k], d.copy));
-        stage_k ^= 1;
+        const uint8_t* src = j.frames[f];
+        if (host_range_pinned(src, span)) {
+          if ((s = upload_pinned(c, d, d.slots[si], src, W, H, j.stride)) != ME_OK) return s;
+        } else {
+          if ((s = ensure_staging(c, d, plane)) != ME_OK) return s;
+          // the copy that last read this staging buffer must be done
+          HIPCHK(c, hipEventSynchronize(d.stage_ev[stage_k]));
+          uint8_t* st = d.stage[stage_k];
+          if (j.stride == W) {
+            memcpy(st, src, plane);
+          } else {
+            for (int y = 0; y < H; y++) memcpy(st + (size_t)y * W, src + (size_t)y * j.stride, W);
+          }
+          if ((s = upload_pinned(c, d, d.slots[si], st, W, H, W)) != ME_OK) return s;
+          HIPCHK(c, hipEventRecord(d.stage_ev[stage_k], d.copy));
+          stage_k ^= 1;
+        }
+        HIPCHK(c, hipEventRecord(d.slot_ready[si], d.copy));
+        slot_of[f] = si;
       }
-      HIPCHK(c, hipEventRecord(d.slot_ready[si], d.copy));
-      slot_of[f] = si;
+      const int sr = slot_of[j.pairs[2 * n]], sc = slot_of[j.pairs[2 * n + 1]];
+      HIPCHK(c, hipStreamWaitEvent(d.stream, d.slot_ready[sr], 0));
+      if (sc != sr) HIPCHK(c, hipStreamWaitEvent(d.stream, d.slot_ready[sc], 0));
+      const size_t o = (size_t)(n - p0) * nb;
+      if (n == n0)
+        base = make_args(d.slots[sr], 0, d.slots[sc], 0, W, H, W, B, j.range, j.cost, 0, nby,
+                         out_mv + 2 * o, out_cost + o);
+      jobs.push_back(SearchJob{d.slots[sr], 0, d.slots[sc], 0, 0, nby, out_mv + 2 * o, out_cost + o});
     }
-    const int sr = slot_of[j.pairs[2 * n]], sc = slot_of[j.pairs[2 * n + 1]];
-    HIPCHK(c, hipStreamWaitEvent(d.stream, d.slot_ready[sr], 0));
-    if (sc != sr) HIPCHK(c, hipStreamWaitEvent(d.stream, d.slot_ready[sc], 0));
-    const size_t o = (size_t)(n - p0) * nb;
-    me::SearchArgs p = make_args(d.slots[sr], 0, d.slots[sc], 0, W, H, W, B, j.range, j.cost, 0,
-                                 nby, out_mv + 2 * o, out_cost + o);
-    {
-      const me_status st = me::attach_scratch(c, d, p);
-      if (st != ME_OK) return st;
-    }
-    if ((s = me::launch_ordered(c, d, p, d.stream)) != ME_OK) return s;
-    if (kAhead <= 8) HIPCHK(c, hipEventRecord(d.pair_ev[(n - p0) % kAhead], d.stream));
-    for (int side = 0; side < 2; side++) {
-      const int f = j.pairs[2 * n + side];
-      if (last_use[f] == n && slot_of[f] >= 0) {
-        const int si = slot_of[f];
-        HIPCHK(c, hipEventRecord(d.slot_free[si], d.stream));
-        free_slots.push_back(si);
-        slot_of[f] = -1;
+    if ((s = me::attach_scratch(c, d, base, false, n1 - n0)) != ME_OK) return s;
+    if ((s = me::launch_jobs_ordered(c, d, base, jobs.data(), n1 - n0, d.stream)) != ME_OK) return s;
+    if (kAhead <= 8) HIPCHK(c, hipEventRecord(d.pair_ev[batch % kAhead], d.stream));
+    for (int n = n0; n < n1; n++)
+      for (int side = 0; side < 2; side++) {
+        const int f = j.pairs[2 * n + side];
+        if (last_use[f] < n1 && slot_of[f] >= 0) {
+          const int si = slot_of[f];
+          HIPCHK(c, hipEventRecord(d.slot_free[si], d.stream));
+          free_slots.push_back(si);
+          slot_of[f] = -1;
+        }
       }
-    }
   }
   HIPCHK(c, hipMemcpyAsync(j.mv_xy + 2 * nb * p0, out_mv, np * nb * 4, hipMemcpyDeviceToHost,
                            d.stream));

@@ -6,7 +6,9 @@ import torch
 import motionestimation_amd as me
 from motionestimation_amd import synth
 
-w, h, npairs = 1920, 1080, int(sys.argv[1]) if len(sys.argv) > 1 else 16
+# args: [npairs [width height]]
+npairs = int(sys.argv[1]) if len(sys.argv) > 1 else 16
+w, h = (int(sys.argv[2]), int(sys.argv[3])) if len(sys.argv) > 3 else (1920, 1080)
 eng = me.Engine(devices=[0])
 pinned = me.pinned_frames(npairs + 1, h, w)
 synth.sequence(w, h, npairs + 1, 1, 3, -3, out=pinned)
@@ -18,4 +20,4 @@ for rep in range(3):
     t0 = time.perf_counter()
     eng.search_pairs(frames, pairs, 16, 32, "sad")
     dt = time.perf_counter() - t0
-    print(f"{npairs} pairs: {dt*1e3:.3f} ms, {npairs/dt:.0f} pairs/s", flush=True)
+    print(f"{w}x{h} {npairs} pairs: {dt*1e3:.3f} ms, {npairs/dt:.0f} pairs/s", flush=True)
