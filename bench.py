@@ -71,8 +71,9 @@ def parse():
                     help="skip the SSD (matrix-core) line beside a SAD run")
     ap.add_argument("--no-stream", action="store_true",
                     help="skip the host frame-pair streaming leg (PCIe-inclusive, not `value`)")
-    ap.add_argument("--cpu-threads", type=int, default=16,
-                    help="threads of the main CPU-baseline leg (the GPU box's CPU share)")
+    ap.add_argument("--cpu-threads", type=int, default=None,
+                    help="threads of the main CPU-baseline leg (default: the process's cgroup "
+                         "CPU quota, cpu.max, rounded down; 16 if none is set)")
     ap.add_argument("--no-4k", action="store_true", help="skip the nested stripe_4k record")
     ap.add_argument("--no-single", action="store_true",
                     help="skip the single_frame record (one frame per launch, for comparison)")
@@ -86,6 +87,9 @@ def parse():
                          "(me_full_search_batch_device) and, in stripe mode, one gather per step")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="nccl = RCCL (production); gloo only to rehearse N ranks on one GPU")
+    ap.add_argument("--comm-timeout-ms", type=int, default=60000,
+                    help="RCCL ranks: bounded wait for a step's searches + gather (me_comm_check); "
+                         "past it the rank aborts its communicator and exits non-zero")
     return ap.parse_args()
 
 
@@ -114,10 +118,48 @@ def exact_absdiffs(w, h, blk, span, row0=0, row1=None):
     return int((nx * bw).sum() * (ny * bh).sum())
 
 
+def cgroup_cpu_quota():
+    """The process's CPU quota from its cgroup: (source text, CPUs as a float,
+    or None when unlimited / unreadable).  cgroup v2: the smallest cpu.max
+    ("<quota> <period>" or "max <period>") from the process's cgroup up to the
+    mounted root; else v1 cpu.cfs_quota_us / cpu.cfs_period_us."""
+    try:
+        with open("/proc/self/cgroup") as f:
+            rel = next((l.strip().split(":", 2)[2] for l in f if l.startswith("0::")), "/")
+    except (OSError, IndexError):
+        rel = "/"
+    best, seen = None, []
+    d = os.path.join("/sys/fs/cgroup", rel.lstrip("/")).rstrip("/")
+    while d.startswith("/sys/fs/cgroup"):
+        try:
+            with open(os.path.join(d, "cpu.max")) as f:
+                raw = f.read().strip()
+            seen.append(f"{d}/cpu.max: {raw}")
+            q, _, p = raw.partition(" ")
+            if q != "max" and p:
+                cpus = int(q) / int(p)
+                best = cpus if best is None else min(best, cpus)
+        except (OSError, ValueError):
+            pass
+        d = os.path.dirname(d)
+    if seen:
+        return "; ".join(seen), best
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            p = int(f.read())
+        return f"cgroup v1 cfs_quota_us {q} period {p}", (q / p if q > 0 else None)
+    except (OSError, ValueError):
+        return None, None
+
+
 def cpu_baselines(ref, cur, blk, span, cost, threads, cands):
     """Rank 0, N=1 only: the oracle restatement (port) timed on the host cores
     on the same frame pair, and the reference's own binary (oracle/_ref/mes,
-    MSE cost, its hard-coded 100-thread pool) when it was built."""
+    MSE cost, its hard-coded 100-thread pool) when it was built.  Returns
+    (record, the port's field (mv, cost) of the whole frame or None): the field
+    is the checker of the timed step's frame 0 (bench.verify_fields)."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import oracle_lib as O
     h, w = ref.shape
@@ -129,14 +171,21 @@ def cpu_baselines(ref, cur, blk, span, cost, threads, cands):
         what = f"block rows {r0}..{min(nby, r0 + 4) - 1} of the"
         cands = sum(_block_candidates(w, h, blk, span, i % nbx, i // nbx)
                     for i in range(begin, end))
+    quota_raw, quota = cgroup_cpu_quota()
+    if threads is None:
+        threads = max(1, int(quota)) if quota else 16
+    field = []
+
     def port(nthreads, variant="", reps=5):
         """median seconds of `reps` oracle searches over blocks [begin, end)"""
         times = []
         for _ in range(reps):
             t0 = time.perf_counter()
-            O.full_search(ref, cur, blk, span, cost, threads=nthreads, begin=begin, end=end,
-                          variant=variant)
+            r = O.full_search(ref, cur, blk, span, cost, threads=nthreads, begin=begin, end=end,
+                              variant=variant)
             times.append(time.perf_counter() - t0)
+            if not field:
+                field.append(r[:2])
         return statistics.median(times)
 
     med = port(threads)
@@ -149,6 +198,7 @@ def cpu_baselines(ref, cur, blk, span, cost, threads, cands):
     affinity = len(os.sched_getaffinity(0))
     out = {"value": cands / med, "unit": "candidates/s", "cores": threads, "kind": "port",
            "cpu_model": cpu_model, "host_cpus": os.cpu_count(), "affinity_cpus": affinity,
+           "cgroup_cpu_quota": {"cpus": quota, "source": quota_raw},
            "sample": f"{what} {w}x{h} B{blk} +-{span} {cost.upper()} frame, "
                      f"oracle/me_oracle.c -O2, {threads} pthreads, median of 5 ({med*1e3:.1f} ms)"}
     # SURVEY §8d's other legs: the port with the reference's 100-thread pool
@@ -187,7 +237,7 @@ def cpu_baselines(ref, cur, blk, span, cost, threads, cands):
                     "kind": "reference", "cost": "mse",
                     "sample": f"unmodified src/cpu (gcc {opt}) on the same frame pair, its own "
                               f"100-thread pool, 'Computation time' median of 3 ({m:.0f} ms)"}
-    return out
+    return out, (field[0] if begin == 0 and end == nbx * nby else None)
 
 
 def host_stream(eng, w, h, blk, span, cost, seed, sx, sy, frame_ms, batch_frame_ms, cands_frame):
@@ -220,10 +270,12 @@ def host_stream(eng, w, h, blk, span, cost, seed, sx, sy, frame_ms, batch_frame_
     return out
 
 
-def single_frame(eng, ref_t, cur_t, blk, span, cost, nb, cands_frame, dev, steps):
+def single_frame(eng, ref_t, cur_t, blk, span, cost, nb, cands_frame, dev, steps, pins):
     """One frame per launch on the same resident pair (HIP events on the
-    launch stream): what batching saves is launch gaps and per-launch tails."""
+    launch stream): what batching saves is launch gaps and per-launch tails.
+    The last timed search's field is checked against pins[0] (ref_t is frame 0)."""
     import torch
+    h, w = ref_t.shape
     mv = torch.empty((nb, 2), dtype=torch.int16, device=dev)
     co = torch.empty(nb, dtype=torch.int32, device=dev)
     for _ in range(3):
@@ -236,15 +288,19 @@ def single_frame(eng, ref_t, cur_t, blk, span, cost, nb, cands_frame, dev, steps
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / steps
+    par = verify_fields(eng, batch_fields(mv, co, 1), None, None, w, h, blk, span, cost,
+                        pins[:1], dev, singles=False)
     return {"value": cands_frame / (ms / 1e3), "unit": "candidates/s", "kernel_ms": ms,
-            "steps": steps, "workload": "one frame per launch (me_full_search_device)"}
+            "steps": steps, "workload": "one frame per launch (me_full_search_device)",
+            "parity": par}
 
 
-def ssd_beside(eng, ref_t, cur_t, blk, span, nb, cands_frame, dev, steps):
+def ssd_beside(eng, ref_t, cur_t, blk, span, nb, cands_frame, dev, steps, pins):
     """The reference's own cost (MSE = SSD / 256) on the step's resident frame
     pairs ([F, H, W] stacks): B = 16 SSD runs on the matrix cores (i8 MFMA), the
     F frames in one batched call (one prepass and one block-major launch).
-    Reported beside `value`; `kernel_ms` is per frame."""
+    Reported beside `value`; `kernel_ms` is per frame.  The last timed batch's
+    fields are checked against the reference's own (pins) and single searches."""
     import torch
     F, h, w = ref_t.shape
     nby = (h + blk - 1) // blk
@@ -262,10 +318,13 @@ def ssd_beside(eng, ref_t, cur_t, blk, span, nb, cands_frame, dev, steps):
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / steps / F
     tops = 2.0 * exact_absdiffs(w, h, blk, span) / (ms / 1e3) / 1e12
+    par = verify_fields(eng, batch_fields(mv, co, F), ref_t, cur_t, w, h, blk, span, "ssd",
+                        pins, dev)
     return {"value": cands_frame / (ms / 1e3), "unit": "candidates/s", "kernel_ms": ms,
             "steps": steps, "frames_per_step": F, "cost": "ssd (reference MSE argmin, bit-exact)",
             "roofline": {"bound": "mfma", "achieved": tops, "peak": I8_PEAK_TOPS,
-                         "unit": "TFLOP/s", "frac": tops / I8_PEAK_TOPS}}
+                         "unit": "TFLOP/s", "frac": tops / I8_PEAK_TOPS},
+            "parity": par}
 
 
 def batch_frames(ref, cur, nframes):
@@ -274,6 +333,103 @@ def batch_frames(ref, cur, nframes):
     same statistics; no extra seconds of synthesis per frame at 4K)."""
     return [(ref, cur) if f == 0 else (np.roll(ref, 37 * f, axis=1), np.roll(cur, 37 * f, axis=1))
             for f in range(nframes)]
+
+
+# ------------------------------------------------------ parity of timed work
+def load_pins(cfg_name, blk, span, cost):
+    """Per-frame SHA-256 pins of batch_frames(named pair of cfg_name) under this
+    search (tests/golden/bench_pins.json, made by tests/golden/make_bench_pins.py:
+    SSD from the unmodified reference, SAD from the oracle restatement), or []."""
+    try:
+        with open(os.path.join(REPO, "tests", "golden", "bench_pins.json")) as f:
+            d = json.load(f).get(f"{cfg_name}_b{blk}_s{span}_{cost}")
+    except (OSError, ValueError):
+        return []
+    return list(d["frame_sha256"]) if d else []
+
+
+def record_stream(mv, cost, w, h, blk, kind):
+    """One frame's field in the pinned record format: SAD int16 mvx, int16 mvy,
+    uint32 sad; SSD the reference's int32 mvx, int32 mvy, float32 mse with
+    mse = (float)SSD / (float)(w*h) of each (edge-clipped) block."""
+    mv = np.ascontiguousarray(mv, np.int16).reshape(-1, 2)
+    cost = np.ascontiguousarray(cost).view(np.uint32).reshape(-1)
+    if kind == "ssd":
+        nbx, nby = (w + blk - 1) // blk, (h + blk - 1) // blk
+        bw = np.minimum(blk, w - np.arange(nbx) * blk)
+        bh = np.minimum(blk, h - np.arange(nby) * blk)
+        area = (bh[:, None] * bw[None, :]).reshape(-1).astype(np.float32)
+        rec = np.empty((len(mv), 3), np.int32)
+        rec[:, :2] = mv
+        rec[:, 2] = (cost.astype(np.float32) / area).view(np.int32)
+        return rec.tobytes()
+    rec = np.empty((len(mv), 8), np.uint8)
+    rec[:, :4] = mv.view(np.uint8).reshape(-1, 4)
+    rec[:, 4:] = cost.view(np.uint8).reshape(-1, 4)
+    return rec.tobytes()
+
+
+def pin_matches(fields, pins, w, h, blk, kind):
+    """Frames of `fields` ([(mv, cost)] in batch order) equal to their pins:
+    (checked, equal)."""
+    import hashlib
+    n = min(len(fields), len(pins))
+    eq = sum(hashlib.sha256(record_stream(mv, co, w, h, blk, kind)).hexdigest() == pins[f]
+             for f, (mv, co) in enumerate(fields[:n]))
+    return n, eq
+
+
+def device_check(eng):
+    """me_device_check after the stream drained: 'ok' or the library's error."""
+    import torch
+    from motionestimation_amd import MEError
+    torch.cuda.synchronize()
+    try:
+        eng.device_check()
+        return "ok"
+    except MEError as e:
+        return str(e)
+
+
+def batch_fields(mv_t, cost_t, F):
+    """[(mv int16 [nb, 2], cost uint32 [nb])] per frame of a batched search's outputs."""
+    mv = mv_t.cpu().numpy().reshape(F, -1, 2)
+    co = cost_t.cpu().numpy().view(np.uint32).reshape(F, -1)
+    return [(mv[f], co[f]) for f in range(F)]
+
+
+def verify_fields(eng, fields, ref_t, cur_t, w, h, blk, span, cost, pins, dev, singles=True):
+    """Parity of a timed step's fields (frame f of the batch = ref_t[f], cur_t[f]):
+    me_device_check clean; each frame equal to a one-frame-per-call search
+    (me_full_search_device: a different launch shape on the same planes); each
+    frame with a pin equal to it (pins: SSD the unmodified reference, SAD the
+    oracle restatement).  Returns the record with "ok"."""
+    import torch
+    out = {"device_check": device_check(eng), "frames": len(fields)}
+    ok = out["device_check"] == "ok"
+    if singles and ref_t is not None:
+        nb = len(fields[0][0])
+        smv = torch.empty((nb, 2), dtype=torch.int16, device=dev)
+        sco = torch.empty(nb, dtype=torch.int32, device=dev)
+        same = 0
+        for f, (mv, co) in enumerate(fields):
+            smv.fill_(-1)
+            eng.full_search_device(ref_t[f], cur_t[f], blk, span, cost, smv, sco)
+            torch.cuda.synchronize()
+            same += bool(np.array_equal(smv.cpu().numpy(), mv) and
+                         np.array_equal(sco.cpu().numpy().view(np.uint32), co))
+        out["single_frame_equal"] = same
+        dc = device_check(eng)
+        ok = ok and same == len(fields) and dc == "ok"
+        if dc != "ok":
+            out["device_check"] = dc
+    n, eq = pin_matches(fields, pins, w, h, blk, cost)
+    out["pinned_frames"], out["pinned_equal"] = n, eq
+    out["pin_source"] = ("tests/golden/bench_pins.json: " +
+                         ("unmodified reference (ref_dump)" if cost == "ssd" else
+                          "oracle/me_oracle.c restatement")) if n else None
+    out["ok"] = bool(ok and eq == n)
+    return out
 
 
 class StripeRun:
@@ -286,7 +442,8 @@ class StripeRun:
     enqueued right after the search on the same stream: the host never waits
     inside the timed region."""
 
-    def __init__(self, eng, dev, world, rank, gloo, frames, blk, span, cost, graph=False):
+    def __init__(self, eng, dev, world, rank, gloo, frames, blk, span, cost, graph=False,
+                 comm_timeout_ms=60000):
         import torch
         import torch.distributed as dist
         from motionestimation_amd import shard
@@ -294,6 +451,7 @@ class StripeRun:
         F = len(frames)
         self.eng, self.dev, self.world, self.rank, self.gloo = eng, dev, world, rank, gloo
         self.w, self.h, self.blk, self.span, self.cost, self.nframes = w, h, blk, span, cost, F
+        self.comm_timeout_ms = comm_timeout_ms
         self.stripes = shard.plan(w, h, blk, span, world)
         # Rank r searches stripe (r + f) % N of frame f: over N frames every
         # rank holds every stripe once, so the ranks' rows balance exactly
@@ -355,6 +513,7 @@ class StripeRun:
                 for k in range(2):
                     self.run_search[k]()
                     self.run_gather[k]()
+                self.drain()
                 torch.cuda.synchronize()
                 try:
                     self.graphs = [eng.capture(stream, lambda k=k: (self.run_search[k](),
@@ -384,6 +543,14 @@ class StripeRun:
             dist.gather(self.recs[k].cpu(), self.bufs[k], dst=0)
         return k
 
+    def drain(self):
+        """Bounded wait for this rank's searches and gathers (RCCL ranks):
+        me_comm_check raises ME_ECOMM (and aborts the communicator, so the
+        stream can drain) when a peer stalled or died, instead of the next
+        synchronize blocking until the driver's timeout."""
+        if self.lib:
+            self.eng.comm_check(self.comm_timeout_ms)
+
     def gather_impl(self):
         if self.world == 1 and not self.lib:
             return None
@@ -398,6 +565,7 @@ class StripeRun:
         import torch
         from motionestimation_amd import shard
         k = self.step()
+        self.drain()
         torch.cuda.synchronize()
         if self.rank != 0:
             return None
@@ -412,7 +580,7 @@ class StripeRun:
         return out
 
 
-def clock_ramp(step, ms, world):
+def clock_ramp(step, ms, world, drain=None):
     """Untimed steps until `ms` of wall time has passed on every rank (ranks
     agree through a MIN all-reduce, so a collective inside the step runs the
     same number of times everywhere).  The GPU's clock ramps up under load:
@@ -426,7 +594,7 @@ def clock_ramp(step, ms, world):
         for _ in range(4):
             step()
         n += 4
-        torch.cuda.synchronize()
+        (drain or torch.cuda.synchronize)()
         el = time.perf_counter() - t0
         if world > 1:
             gloo = dist.get_backend() == "gloo"
@@ -439,17 +607,22 @@ def clock_ramp(step, ms, world):
     return n
 
 
-def timed(step, steps, warmup, world, finish=None, ramp_ms=0):
+def timed(step, steps, warmup, world, finish=None, ramp_ms=0, drain=None):
     """The clock ramp (clock_ramp), W untimed steps, then K steps between
     barrier + synchronize; returns (max-over-ranks wall seconds, max-over-ranks
-    ms per step on the current stream from one HIP event pair around the region)."""
+    ms per step on the current stream from one HIP event pair around the region).
+    drain: a bounded wait for the stream run before each synchronize (RCCL
+    ranks: me_comm_check, which raises ME_ECOMM instead of hanging when a peer
+    rank stalled or died)."""
     import torch
     import torch.distributed as dist
-    clock_ramp(step, ramp_ms, world)
+    drain = drain or (lambda: None)
+    clock_ramp(step, ramp_ms, world, lambda: (drain(), torch.cuda.synchronize()))
     for _ in range(warmup):
         step()
     if finish:
         finish()
+    drain()
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
@@ -462,6 +635,7 @@ def timed(step, steps, warmup, world, finish=None, ramp_ms=0):
     if finish:
         finish()
     ev1.record()
+    drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -476,31 +650,63 @@ def timed(step, steps, warmup, world, finish=None, ramp_ms=0):
     return elapsed, kern_ms
 
 
-def stripe_parity(eng, sr, frames, dev):
-    """Rank 0: the gathered stripe fields of every frame of the step equal one
-    batched full-frame search on one GPU (not timed)."""
+def all_ranks_ok(ok, world):
+    """True on every rank iff `ok` is true on every rank (MIN all-reduce)."""
+    if world == 1:
+        return bool(ok)
+    import torch
+    import torch.distributed as dist
+    gloo = dist.get_backend() == "gloo"
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32,
+                     device="cpu" if gloo else torch.device("cuda", torch.cuda.current_device()))
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(int(t[0]))
+
+
+def stripe_parity(eng, sr, frames, dev, pins):
+    """Parity of a stripe run's last step (not timed).  Every rank: its
+    searches' me_device_check is clean.  Rank 0: the gathered stripe fields of
+    every frame of the step equal one batched full-frame search on one GPU and
+    their pins (frame f of the step = batch_frames' frame f).  Returns the
+    record on rank 0 ({"ok"} elsewhere); "ok" covers every rank."""
     import torch
     import motionestimation_amd as me
     fields = sr.gathered_fields()
-    if sr.rank != 0:
-        return None
-    h, w = frames[0][0].shape
-    nb = me.num_blocks(w, h, sr.blk)
-    F = len(frames)
-    fmv = torch.empty((F * nb, 2), dtype=torch.int16, device=dev)
-    fco = torch.empty(F * nb, dtype=torch.int32, device=dev)
-    eng.search_batch_device(torch.from_numpy(np.stack([r for r, _ in frames])).to(dev), 0,
-                            torch.from_numpy(np.stack([c for _, c in frames])).to(dev), 0, w, h,
-                            sr.blk, sr.span, sr.cost, 0, (h + sr.blk - 1) // sr.blk, fmv, fco)
-    torch.cuda.synchronize()
-    fmv, fco = fmv.cpu().numpy(), fco.cpu().numpy().view(np.uint32)
-    return all(np.array_equal(gmv, fmv[f * nb:(f + 1) * nb]) and
-               np.array_equal(gcost, fco[f * nb:(f + 1) * nb])
-               for f, (gmv, gcost) in enumerate(fields))
+    dc = device_check(eng)
+    rec = None
+    if sr.rank == 0:
+        h, w = frames[0][0].shape
+        nb = me.num_blocks(w, h, sr.blk)
+        F = len(frames)
+        fmv = torch.empty((F * nb, 2), dtype=torch.int16, device=dev)
+        fco = torch.empty(F * nb, dtype=torch.int32, device=dev)
+        eng.search_batch_device(torch.from_numpy(np.stack([r for r, _ in frames])).to(dev), 0,
+                                torch.from_numpy(np.stack([c for _, c in frames])).to(dev), 0, w,
+                                h, sr.blk, sr.span, sr.cost, 0, (h + sr.blk - 1) // sr.blk, fmv,
+                                fco)
+        torch.cuda.synchronize()
+        batch = batch_fields(fmv, fco, F)
+        same = sum(bool(np.array_equal(g[0], b[0]) and np.array_equal(g[1], b[1]))
+                   for g, b in zip(fields, batch))
+        n, eq = pin_matches(fields, pins, w, h, sr.blk, sr.cost)
+        rec = {"frames": F, "batched_equal": same, "pinned_frames": n, "pinned_equal": eq,
+               "pin_source": "tests/golden/bench_pins.json" if n else None}
+        ok = dc == "ok" and same == F and eq == n
+    else:
+        ok = dc == "ok"
+    ok = all_ranks_ok(ok, sr.world)
+    if rec is not None:
+        rec["device_check"] = dc if sr.world == 1 else ("ok on every rank" if ok else
+                                                        f"rank 0: {dc} (see every rank's stderr)")
+    if dc != "ok":
+        print(f"bench.py: rank {sr.rank}: {dc}", file=sys.stderr)
+    rec = rec if rec is not None else {}
+    rec["ok"] = ok
+    return rec
 
 
 def stripe_record(eng, dev, world, rank, gloo, cfg_name, cost, steps, warmup, nframes,
-                  graph=False, ramp_ms=0):
+                  graph=False, ramp_ms=0, comm_timeout_ms=60000):
     """Nested record: a BASELINE config in stripe mode on the same ranks."""
     import motionestimation_amd as me
     from motionestimation_amd import synth
@@ -508,9 +714,9 @@ def stripe_record(eng, dev, world, rank, gloo, cfg_name, cost, steps, warmup, nf
     w, h, seed, sx, sy = synth.CONFIGS[cfg]
     frames = batch_frames(*synth.frame_pair(w, h, seed, sx, sy), nframes)
     cands = me.candidate_count(w, h, blk, span)
-    sr = StripeRun(eng, dev, world, rank, gloo, frames, blk, span, cost, graph)
-    elapsed, kern_ms = timed(sr.step, steps, warmup, world, ramp_ms=ramp_ms)
-    parity = stripe_parity(eng, sr, frames, dev)
+    sr = StripeRun(eng, dev, world, rank, gloo, frames, blk, span, cost, graph, comm_timeout_ms)
+    elapsed, kern_ms = timed(sr.step, steps, warmup, world, ramp_ms=ramp_ms, drain=sr.drain)
+    parity = stripe_parity(eng, sr, frames, dev, load_pins(cfg_name, blk, span, cost))
     return {"value": cands * nframes * steps / elapsed, "unit": "candidates/s",
             "frames_per_s": nframes * steps / elapsed, "ms_per_step": elapsed / steps * 1e3,
             "kernel_ms": kern_ms, "steps": steps, "warmup": warmup, "n_gpus": world,
@@ -518,7 +724,8 @@ def stripe_record(eng, dev, world, rank, gloo, cfg_name, cost, steps, warmup, nf
             "workload": f"{w}x{h} Y, {blk}x{blk} blocks, full search +-{span}, {cost.upper()}, "
                         f"{nframes} frames per step, each in row stripes over the ranks; one "
                         "batched search and one RCCL gather per step",
-            "candidates_per_frame": cands, "stripe_gather_parity": parity,
+            "candidates_per_frame": cands,
+            "stripe_gather_parity": parity["ok"] if parity else None, "parity": parity,
             "gather": sr.gather_impl()}
 
 
@@ -637,10 +844,14 @@ def main():
     # a one-rank group included
     launched = "WORLD_SIZE" in os.environ
     if launched:
+        # torch's own collectives (barriers, the ramp's MIN, the result MAX)
+        # fail after this instead of the default 10 minutes
+        import datetime
+        tmo = datetime.timedelta(seconds=max(60, 3 * args.comm_timeout_ms // 1000))
         if gloo:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=tmo)
         else:
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, timeout=tmo)
 
     import motionestimation_amd as me
     from motionestimation_amd import synth
@@ -654,6 +865,7 @@ def main():
     mode = args.mode if args.mode != "auto" else ("frames" if world == 1 else "stripe")
     F = args.frames_per_step
     parity = None
+    pins = load_pins(args.config, blk, span, args.cost)
     if mode == "frames":
         # rank r: its own batch of F frame pairs (same size; seed varies), all F
         # searched in one launch per step (me_full_search_batch_device)
@@ -670,13 +882,21 @@ def main():
         # launched on (torch's current stream) around the whole timed region,
         # / K (per-step event pairs would stretch the back-to-back launches).
         elapsed, kern_ms = timed(step, args.steps, args.warmup, world, ramp_ms=args.ramp_ms)
+        # The timed step's own output (mv_t / cost_t hold the last step's
+        # fields): device check, one-frame-per-call searches, and the pins of
+        # this batch (rank 0: its frames are the pinned batch_frames).
+        parity = verify_fields(eng, batch_fields(mv_t, cost_t, F), ref_t, cur_t, w, h, blk, span,
+                               args.cost, pins if rank == 0 else [], dev)
+        parity["ok"] = all_ranks_ok(parity["ok"], world)
     else:
         ref, cur = synth.frame_pair(w, h, seed, sx, sy)
         frames = batch_frames(ref, cur, F)
-        sr = StripeRun(eng, dev, world, rank, gloo, frames, blk, span, args.cost, args.graph)
+        sr = StripeRun(eng, dev, world, rank, gloo, frames, blk, span, args.cost, args.graph,
+                       args.comm_timeout_ms)
         units_per_step = cands_frame * F
-        elapsed, kern_ms = timed(sr.step, args.steps, args.warmup, world, ramp_ms=args.ramp_ms)
-        parity = stripe_parity(eng, sr, frames, dev)
+        elapsed, kern_ms = timed(sr.step, args.steps, args.warmup, world, ramp_ms=args.ramp_ms,
+                                 drain=sr.drain)
+        parity = stripe_parity(eng, sr, frames, dev, pins)
 
     value = units_per_step * args.steps / elapsed
     # Roofline of the dominant kernel: algorithmic HBM bytes per
@@ -763,27 +983,41 @@ def main():
                             "hbm": {k: hbm[k] for k in ("achieved", "peak", "unit", "frac",
                                                         "algorithmic_bytes", "per",
                                                         "frames_per_launch", "launch_ms")}}
+    # Parity of every measured leg: the line verifies the work
+    # its own timed regions did; `parity` is false and the exit status
+    # non-zero if any leg's fields differ or a kernel reported ME_EDEVICE.
+    legs = {"timed_step": parity}
+    if mode == "stripe":
+        line["stripe_gather_parity"] = parity.get("batched_equal") == F if rank == 0 else None
+        line["config"]["gather"] = sr.gather_impl()
     if rank == 0 and world == 1 and mode == "frames" and F > 1 and not args.no_single:
         # the same search one frame per launch (me_full_search_device), for
         # comparison: the batch's only difference is launches per frame
         line["single_frame"] = single_frame(eng, ref_t[0], cur_t[0], blk, span, args.cost, nb,
-                                            cands_frame, dev, min(args.steps * F, 100))
+                                            cands_frame, dev, min(args.steps * F, 100), pins)
+        legs["single_frame"] = line["single_frame"]["parity"]
     if (rank == 0 and world == 1 and mode == "frames" and args.cost == "sad"
             and blk == 16 and not args.no_ssd):
         line["ssd_mfma"] = ssd_beside(eng, ref_t, cur_t, blk, span, nb, cands_frame, dev,
-                                      min(args.steps, 20))
-    if parity is not None:
-        line["stripe_gather_parity"] = parity
-        line["config"]["gather"] = sr.gather_impl()
+                                      min(args.steps, 20), load_pins(args.config, blk, span, "ssd"))
+        legs["ssd_mfma"] = line["ssd_mfma"]["parity"]
     if rank == 0 and world == 1 and not args.no_cpu:
-        line["cpu_baseline"] = cpu_baselines(ref, cur, blk, span, args.cost, args.cpu_threads,
-                                             cands_frame)
+        line["cpu_baseline"], field = cpu_baselines(ref, cur, blk, span, args.cost,
+                                                    args.cpu_threads, cands_frame)
+        if field is not None and mode == "frames":
+            # the oracle's field of the CPU leg, run live on this box, against
+            # frame 0 of the timed step (frame 0 = this ref/cur pair)
+            mv0, co0 = batch_fields(mv_t, cost_t, F)[0]
+            eq = bool(np.array_equal(field[0], mv0) and np.array_equal(field[1], co0))
+            legs["oracle_frame0"] = {"ok": eq, "what": "cpu_baseline's oracle field of frame 0 "
+                                                       "== the timed step's frame 0"}
     if not args.no_4k and args.cost in ("sad", "ssd"):
         # BASELINE configs[3] (4K +-64), the config north_star's 8-GPU split is
         # quoted on, in stripe mode on the same ranks (at N = 1: the denominator)
         rec4k = stripe_record(eng, dev, world, rank, gloo, "4k", args.cost,
                               min(args.steps, 20), min(args.warmup, 3), F, args.graph,
-                              min(args.ramp_ms, 30.0))
+                              min(args.ramp_ms, 30.0), args.comm_timeout_ms)
+        legs["stripe_4k"] = rec4k["parity"]
         if rank == 0:
             line["stripe_4k"] = rec4k
     if rank == 0 and world == 1 and mode == "frames" and not args.no_stream:
@@ -791,11 +1025,19 @@ def main():
         one = line.get("single_frame", {}).get("kernel_ms", kern_ms / F)
         line["host_stream"] = host_stream(eng, w, h, blk, span, args.cost, seed, sx, sy,
                                           one, kern_ms / F, cands_frame)
+    ok = all(leg["ok"] for leg in legs.values())
+    line["parity"] = ok
+    line["parity_legs"] = legs
     if rank == 0:
         print(json.dumps(line), file=json_out, flush=True)
     eng.close()
     if launched:
         dist.destroy_process_group()
+    if not ok:
+        bad = [k for k, leg in legs.items() if not leg["ok"]]
+        print(f"bench.py: rank {rank}: parity FAILED in {bad}: {json.dumps(legs)}",
+              file=sys.stderr)
+        sys.exit(1)
 
 
 if __name__ == "__main__":

@@ -205,12 +205,29 @@ me_status me_comm_init(me_ctx* ctx, const void* id, int n_ranks, int rank);
  * `stream` (a hipStream_t) after the work already on it; asynchronous. */
 me_status me_gather_device(me_ctx* ctx, const void* d_send, size_t bytes, void* d_recv,
                            void* stream);
+/* Failure detection for the exchange (the reference checks CUDA
+ * errors once, at exit: src/gpu/main_mse.cu:275-276).  Waits at most
+ * timeout_ms for the work enqueued so far on `stream` (the rank's searches and
+ * gathers) while polling RCCL's asynchronous error (ncclCommGetAsyncError).
+ * ME_OK: the stream drained and RCCL reports no error.  ME_ECOMM: RCCL
+ * reported an error, or the wait timed out (a peer rank stalled or died); the
+ * communicator is then aborted (ncclCommAbort), so this rank's RCCL kernels
+ * return and the stream can be synchronised instead of hanging, and every
+ * later me_gather_device / me_comm_check on the context fails with ME_ECOMM.
+ * me_last_error names the cause.  The multi-device me_full_search waits the
+ * same way (ME_COMM_TIMEOUT_MS) and rebuilds its group after a failure. */
+#define ME_COMM_TIMEOUT_MS 60000
+me_status me_comm_check(me_ctx* ctx, void* stream, int timeout_ms);
 
 /* ME_EDEVICE if a search kernel of this context reported a broken in-kernel
  * invariant (a bounded wait that expired: the kernel ends instead of hanging
  * the GPU, and that search's MV field is invalid) since the last check; the
  * report is cleared.  Call after the searches' streams have finished.
- * me_full_search, me_find_best_blocks and me_search_pairs check on their own. */
+ * me_full_search, me_find_best_blocks and me_search_pairs check on their own;
+ * the word is per device, so such a synchronous call also fails with
+ * ME_EDEVICE when an earlier, still unchecked asynchronous search on the
+ * device broke its invariant, and the report stays pending for that
+ * search's own me_device_check as well. */
 me_status me_device_check(me_ctx* ctx);
 
 /* ---- captured steps (hipGraph) ----

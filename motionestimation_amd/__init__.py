@@ -5,7 +5,8 @@ The compute path is libme_hip.so (HIP kernels for gfx950 behind the C ABI of
 include/me.h); this package is the host-side mirror of the reference's
 interface over that ABI.  There is no CPU fallback.
 """
-from ._lib import ME_COST_SAD, ME_COST_SSD, ME_COST_SSIM, MEError, build  # noqa: F401
+from ._lib import (ME_COST_SAD, ME_COST_SSD, ME_COST_SSIM, ME_ECOMM, ME_EDEVICE,  # noqa: F401
+                   MEError, build)
 from .engine import (Engine, candidate_count, num_blocks, pinned_frames,  # noqa: F401
                      plan_stripes, set_kernel_path, version)
 from . import io  # noqa: F401

@@ -17,6 +17,7 @@ CSRC = os.path.join(PKG, "csrc")
 
 ME_OK, ME_EINVAL, ME_ENOMEM, ME_EDEVICE, ME_ECOMM, ME_EUNSUPPORTED, ME_EIO = range(7)
 ME_COMM_ID_BYTES = 128  # include/me.h (sizeof ncclUniqueId)
+ME_COMM_TIMEOUT_MS = 60000
 ME_YUV_LUMA, ME_YUV_I420 = 0, 1
 ME_COST_SSD, ME_COST_SAD, ME_COST_SSIM = 0, 1, 2
 ME_PATH_AUTO, ME_PATH_VALU, ME_PATH_MFMA_TILES = 0, 1, 2
@@ -52,6 +53,7 @@ _SIGS = {
     "me_comm_init": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
     "me_gather_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
                                         ctypes.c_void_p, ctypes.c_void_p]),
+    "me_comm_check": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "me_device_check": (ctypes.c_int, [ctypes.c_void_p]),
     "me_capture_begin": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "me_capture_end": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p,

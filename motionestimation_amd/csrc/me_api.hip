@@ -13,6 +13,7 @@
 #include <string.h>
 
 #include <atomic>
+#include <chrono>
 #include <new>
 #include <thread>
 #include <vector>
@@ -284,12 +285,102 @@ me_status device_status(me_ctx* c, Dev& d, hipStream_t s) {
   HIPCHK(c, hipMemcpyAsync(&w, d.sched + SCHED_ERR, 4, hipMemcpyDeviceToHost, s));
   HIPCHK(c, hipStreamSynchronize(s));
   if (w) {
+    // The word is per device, so it may also hold the report of an earlier
+    // asynchronous search that nobody checked yet: keep it for that caller's
+    // me_device_check as well (include/me.h).
+    d.err_pending = w;
     HIPCHK(c, hipMemsetAsync(d.sched + SCHED_ERR, 0, 4, s));
     HIPCHK(c, hipStreamSynchronize(s));
     return fail(c, ME_EDEVICE, "device %d: a search kernel's bounded wait expired (code %u): "
-                "the MV field of that search is invalid", d.id, w);
+                "the MV field of this or an earlier unchecked search on the device is invalid",
+                d.id, w);
   }
   return ME_OK;
+}
+
+// ------------------------------------------------------------ host workers
+Workers::Workers(int n) {
+  th_.reserve(n);
+  for (int i = 0; i < n; i++) th_.emplace_back(&Workers::loop, this, i);
+}
+
+Workers::~Workers() {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    stop_ = true;
+  }
+  go_.notify_all();
+  for (auto& t : th_) t.join();
+}
+
+void Workers::loop(int i) {
+  unsigned long long seen = 0;
+  for (;;) {
+    const std::function<void(int)>* fn;
+    int n;
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      go_.wait(lk, [&] { return stop_ || gen_ != seen; });
+      if (stop_) return;
+      seen = gen_;
+      fn = fn_;
+      n = n_;
+    }
+    if (i < n) (*fn)(i);
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      if (--pending_ == 0) done_.notify_one();
+    }
+  }
+}
+
+void Workers::run(int n, const std::function<void(int)>& fn) {
+  std::unique_lock<std::mutex> lk(mu_);
+  fn_ = &fn;
+  n_ = n;
+  pending_ = (int)th_.size();
+  gen_++;
+  go_.notify_all();
+  done_.wait(lk, [&] { return pending_ == 0; });
+  fn_ = nullptr;
+}
+
+Workers* workers(me_ctx* c) {
+  if (!c->pool) {
+    try {
+      c->pool = new Workers((int)c->devs.size());
+    } catch (...) {  // std::system_error: no thread could be started
+      c->pool = nullptr;
+    }
+  }
+  return c->pool;
+}
+
+// ------------------------------------------------- RCCL failure detection
+me_status wait_comm(me_ctx* c, hipStream_t s, hipEvent_t ev, ncclComm_t comm, int timeout_ms) {
+  HIPCHK(c, hipEventRecord(ev, s));
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int spins = 0;; spins++) {
+    const hipError_t q = hipEventQuery(ev);
+    ncclResult_t ar = ncclSuccess;
+    if (comm && ncclCommGetAsyncError(comm, &ar) == ncclSuccess && ar != ncclSuccess &&
+        ar != ncclInProgress)
+      return fail(c, ME_ECOMM, "RCCL reported an asynchronous error: %s (%s)",
+                  ncclGetErrorString(ar), comm ? ncclGetLastError(comm) : "");
+    if (q == hipSuccess) return ME_OK;
+    if (q != hipErrorNotReady) return fail(c, ME_EDEVICE, "stream query: %s", hipGetErrorString(q));
+    const auto ms = std::chrono::duration_cast<std::chrono::milliseconds>(
+                        std::chrono::steady_clock::now() - t0).count();
+    if (ms >= timeout_ms)
+      return fail(c, ME_ECOMM, "the collective did not complete within %d ms (a rank stalled "
+                  "or died); the communicator is aborted", timeout_ms);
+    // spin for the first ~0.1 ms (the usual case: the gather is microseconds
+    // from done), then poll every 50 us
+    if (spins < 200)
+      std::this_thread::yield();
+    else
+      std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
 }
 
 }  // namespace me
@@ -369,16 +460,15 @@ me_status multi_search(me_ctx* c, const uint8_t* ref, const uint8_t* cur, int wi
   const size_t rec_bytes = max_blocks * 8;
 
   {
+    // one persistent host thread per device (me::Workers), not threads per call
+    me::Workers* pool = me::workers(c);
+    if (!pool) return fail(c, ME_ENOMEM, "host worker threads");
     std::vector<me_ctx> errs(n);
     std::vector<me_status> st(n, ME_OK);
-    std::vector<std::thread> th;
-    th.reserve(n);
-    for (int i = 0; i < n; i++)
-      th.emplace_back([&, i]() {
-        st[i] = stripe_upload_launch(&errs[i], c->devs[i], ref, cur, width, height, stride, blk,
-                                     range, cost, bounds[i], bounds[i + 1], max_blocks);
-      });
-    for (auto& t : th) t.join();
+    pool->run(n, [&](int i) {
+      st[i] = stripe_upload_launch(&errs[i], c->devs[i], ref, cur, width, height, stride, blk,
+                                   range, cost, bounds[i], bounds[i + 1], max_blocks);
+    });
     for (int i = 0; i < n; i++)
       if (st[i] != ME_OK) return fail(c, st[i], "device %d: %s", c->devs[i].id, errs[i].err);
   }
@@ -394,6 +484,20 @@ me_status multi_search(me_ctx* c, const uint8_t* ref, const uint8_t* cur, int wi
                             c->comms[i], d.stream));
     }
     NCCLCHK(c, ncclGroupEnd());
+    // Bounded wait on every device's gather: a device that stalls (or an RCCL
+    // error) aborts the group instead of blocking this call forever; the next
+    // search builds a new one.
+    for (int i = 0; i < n; i++) {
+      Dev& d = c->devs[i];
+      HIPCHK(c, hipSetDevice(d.id));
+      s = me::wait_comm(c, d.stream, d.search_ev, c->comms[i], ME_COMM_TIMEOUT_MS);
+      if (s != ME_OK) {
+        for (int k = 0; k < n; k++) (void)ncclCommAbort(c->comms[k]);
+        delete[] c->comms;
+        c->comms = nullptr;
+        return s;
+      }
+    }
   } else {
     // Repeated device ids: stripes share a device; device copies stand in for the gather.
     for (int i = 0; i < n; i++) {
@@ -525,11 +629,35 @@ me_status me_comm_init(me_ctx* c, const void* id, int n_ranks, int rank) {
 me_status me_gather_device(me_ctx* c, const void* d_send, size_t bytes, void* d_recv,
                            void* stream) {
   if (!c) return ME_EINVAL;
+  if (c->comm_aborted)
+    return fail(c, ME_ECOMM, "the communicator was aborted by me_comm_check (a failed exchange)");
   if (!c->rank_comm) return fail(c, ME_EINVAL, "me_comm_init was not called");
   if (!d_send || (c->comm_rank == 0 && !d_recv)) return fail(c, ME_EINVAL, "null buffer");
   NCCLCHK(c, ncclGather(d_send, c->comm_rank == 0 ? d_recv : nullptr, bytes, ncclUint8, 0,
                         c->rank_comm, reinterpret_cast<hipStream_t>(stream)));
   return ME_OK;
+}
+
+me_status me_comm_check(me_ctx* c, void* stream, int timeout_ms) {
+  if (!c) return ME_EINVAL;
+  if (c->comm_aborted)
+    return fail(c, ME_ECOMM, "the communicator was aborted by an earlier me_comm_check");
+  if (!c->rank_comm) return fail(c, ME_EINVAL, "me_comm_init was not called");
+  if (timeout_ms < 0) return fail(c, ME_EINVAL, "timeout_ms %d", timeout_ms);
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  HIPCHK(c, hipSetDevice(c->devs[0].id));
+  if (!c->comm_ev) HIPCHK(c, hipEventCreateWithFlags(&c->comm_ev, hipEventDisableTiming));
+  me_status s = me::wait_comm(c, (hipStream_t)stream, c->comm_ev, c->rank_comm, timeout_ms);
+  if (s == ME_ECOMM) {
+    // Abort: RCCL's kernels on this rank return, so the stream (and every
+    // stream synchronisation after it) can finish instead of hanging.
+    (void)ncclCommAbort(c->rank_comm);
+    c->rank_comm = nullptr;
+    c->comm_aborted = true;
+  }
+  (void)hipSetDevice(prev);
+  return s;
 }
 
 me_status me_device_check(me_ctx* c) {
@@ -544,10 +672,12 @@ me_status me_device_check(me_ctx* c) {
       s = fail(c, ME_EDEVICE, "device %d: reading the invariant word failed", d.id);
       break;
     }
-    if (w) {
-      (void)hipMemset(d.sched + me::SCHED_ERR, 0, 4);
-      s = fail(c, ME_EDEVICE, "device %d: a search kernel's bounded wait expired (code %u): "
-               "the MV field of that search is invalid", d.id, w);
+    if (w || d.err_pending) {
+      if (w) (void)hipMemset(d.sched + me::SCHED_ERR, 0, 4);
+      s = fail(c, ME_EDEVICE, "device %d: a search kernel's bounded wait expired (code %u%s): "
+               "the MV field of that search is invalid", d.id, w ? w : d.err_pending,
+               w ? "" : ", first reported to a synchronous call");
+      d.err_pending = 0;
       break;
     }
   }
@@ -610,7 +740,10 @@ void me_graph_destroy(me_graph* g) {
 
 void me_destroy(me_ctx* c) {
   if (!c) return;
+  delete c->pool;  // joins the idle workers
+  c->pool = nullptr;
   if (c->rank_comm) ncclCommDestroy(c->rank_comm);
+  if (c->comm_ev) (void)hipEventDestroy(c->comm_ev);
   if (c->comms) {
     for (size_t i = 0; i < c->devs.size(); i++) ncclCommDestroy(c->comms[i]);
     delete[] c->comms;

@@ -7,6 +7,10 @@
 #include <stdarg.h>
 #include <stdint.h>
 
+#include <condition_variable>
+#include <functional>
+#include <mutex>
+#include <thread>
 #include <vector>
 
 #include "me.h"
@@ -55,7 +59,44 @@ struct Dev {
   hipEvent_t pair_ev[8] = {};  // search of pair n done: bounds how far the host runs ahead
   uint8_t* pair_out = nullptr;  // [pairs][nblocks] mv records, then [pairs][nblocks] costs
   size_t pair_out_cap = 0;
+  // An invariant report that a synchronous entry point read (and cleared on
+  // the device) on behalf of earlier asynchronous searches: me_device_check
+  // still reports it once (device_status sets it, me_device_check clears it).
+  uint32_t err_pending = 0;
 };
+
+// Persistent host workers, one per context device (multi-device searches and
+// pair runs): started on first use, joined by me_destroy.  run(n, fn) calls
+// fn(i) on worker i for i < n and returns when all have finished; one caller
+// at a time (a context is used by one host thread at a time, include/me.h).
+class Workers {
+ public:
+  explicit Workers(int n);
+  ~Workers();
+  int size() const { return (int)th_.size(); }
+  void run(int n, const std::function<void(int)>& fn);
+
+ private:
+  void loop(int i);
+  std::vector<std::thread> th_;
+  std::mutex mu_;
+  std::condition_variable go_, done_;
+  const std::function<void(int)>* fn_ = nullptr;
+  unsigned long long gen_ = 0;
+  int n_ = 0, pending_ = 0;
+  bool stop_ = false;
+};
+
+// The context's workers, created with one thread per device on first use
+// (nullptr if a thread could not be started).
+Workers* workers(me_ctx* c);
+
+// Wait, bounded, for the work enqueued so far on stream s of device d (one
+// that ends in RCCL collectives on `comm`), polling the stream and the
+// communicator's asynchronous error.  ME_OK when the stream drained;
+// ME_ECOMM when RCCL reported an error or timeout_ms passed (a peer stalled or
+// died): the caller aborts the communicator.  ev: a scratch event of d.
+me_status wait_comm(me_ctx* c, hipStream_t s, hipEvent_t ev, ncclComm_t comm, int timeout_ms);
 
 // Free the pair pipeline's buffers and events of one device (me_destroy).
 void release_pipeline(Dev& d);
@@ -114,6 +155,9 @@ struct me_ctx {
   ncclComm_t* comms = nullptr;
   ncclComm_t rank_comm = nullptr;  // me_comm_init: one rank of a multi-process group
   int comm_ranks = 0, comm_rank = -1;
+  bool comm_aborted = false;       // me_comm_check aborted rank_comm (failure detected)
+  hipEvent_t comm_ev = nullptr;    // me_comm_check's marker on the checked stream
+  me::Workers* pool = nullptr;     // me::workers(): persistent per-device host threads
   char err[512] = {0};
 };
 

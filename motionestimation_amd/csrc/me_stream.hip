@@ -324,16 +324,16 @@ me_status me_search_pairs(me_ctx* c, const uint8_t* const* frames, int n_frames,
                     mv_xy, block_cost};
   const int nd = (int)c->devs.size();
   if (nd == 1) return me::run_pairs(c, c->devs[0], job, 0, n_pairs);
-  // One host thread per device, contiguous runs of pairs (shared frames of
+  // One persistent host worker per device, contiguous runs of pairs (shared frames of
   // neighbouring pairs stay on one device); errors land in per-thread contexts.
+  me::Workers* pool = me::workers(c);
+  if (!pool) return me::fail(c, ME_ENOMEM, "host worker threads");
   std::vector<me_ctx> errs(nd);
   std::vector<me_status> st(nd, ME_OK);
-  std::vector<std::thread> th;
-  for (int i = 0; i < nd; i++) {
+  pool->run(nd, [&](int i) {
     const int p0 = (int)((long)n_pairs * i / nd), p1 = (int)((long)n_pairs * (i + 1) / nd);
-    th.emplace_back([&, i, p0, p1]() { st[i] = me::run_pairs(&errs[i], c->devs[i], job, p0, p1); });
-  }
-  for (auto& t : th) t.join();
+    st[i] = me::run_pairs(&errs[i], c->devs[i], job, p0, p1);
+  });
   for (int i = 0; i < nd; i++)
     if (st[i] != ME_OK) return me::fail(c, st[i], "device %d: %s", c->devs[i].id, errs[i].err);
   return ME_OK;

@@ -272,6 +272,14 @@ class Engine:
             recv_t.data_ptr() if recv_t is not None else None, st), self._h)
 
 
+    def comm_check(self, timeout_ms: int = _lib.ME_COMM_TIMEOUT_MS, stream=None) -> None:
+        """Bounded wait for the work on `stream` (default: torch's current
+        stream) with RCCL failure detection (me_comm_check): raises MEError
+        (ME_ECOMM) on an RCCL error or when timeout_ms passed; the communicator
+        is then aborted."""
+        st = stream if stream is not None else _current_stream()
+        check(_lib.lib().me_comm_check(self._h, st, int(timeout_ms)), self._h)
+
     def device_check(self) -> None:
         """Raise MEError (ME_EDEVICE) if a search kernel reported a broken
         in-kernel invariant since the last check (call after synchronising)."""
@@ -284,11 +292,16 @@ class Engine:
         searches once uncaptured first (they size the context's scratch)."""
         L = _lib.lib()
         check(L.me_capture_begin(self._h, stream), self._h)
+        g = ctypes.c_void_p()
         try:
             enqueue()
-        finally:
-            g = ctypes.c_void_p()
-            st = L.me_capture_end(self._h, stream, ctypes.byref(g))
+        except BaseException:
+            # end the capture (the stream must leave capture mode) and drop the
+            # graph it made; the enqueue's exception is the one that propagates
+            if L.me_capture_end(self._h, stream, ctypes.byref(g)) == _lib.ME_OK and g:
+                L.me_graph_destroy(g)
+            raise
+        st = L.me_capture_end(self._h, stream, ctypes.byref(g))
         check(st, self._h)
         gr = Graph(self, g)
         if not hasattr(self, "_graphs"):

@@ -102,6 +102,45 @@ def test_library_communicator_one_rank():
         assert torch.equal(dst[0], src)
 
 
+def test_comm_check_one_rank():
+    """me_comm_check (failure detection of the exchange): clean after a
+    gather on a one-rank group; when the stream's work outlasts the timeout it
+    returns ME_ECOMM and aborts the communicator, the stream still drains, and
+    every later gather or check fails loudly instead of hanging."""
+    import torch
+    with me.Engine(devices=[0]) as eng:
+        with pytest.raises(me.MEError):  # no communicator yet
+            eng.comm_check(1000)
+        eng.comm_init(eng.comm_unique_id(), 1, 0)
+        src = torch.arange(4096, dtype=torch.int32, device="cuda")
+        dst = torch.zeros((1, 4096), dtype=torch.int32, device="cuda")
+        eng.gather_device(src, dst)
+        eng.comm_check(10_000)
+        assert torch.equal(dst[0], src)
+        # ~10 ms of searches ahead of the check, and a zero timeout: a "stalled" exchange
+        w, h = 1920, 1080
+        ref = torch.randint(0, 256, (16, h, w), dtype=torch.uint8, device="cuda")
+        cur = torch.randint(0, 256, (16, h, w), dtype=torch.uint8, device="cuda")
+        nb = me.num_blocks(w, h, 16)
+        mv = torch.empty((16 * nb, 2), dtype=torch.int16, device="cuda")
+        co = torch.empty(16 * nb, dtype=torch.int32, device="cuda")
+        torch.cuda.synchronize()
+        for _ in range(10):
+            eng.search_batch_device(ref, 0, cur, 0, w, h, 16, 32, "sad", 0, (h + 15) // 16, mv, co)
+        eng.gather_device(src, dst)
+        with pytest.raises(me.MEError) as e:
+            eng.comm_check(0)
+        assert e.value.status == me.ME_ECOMM and "aborted" in str(e.value)
+        torch.cuda.synchronize()  # the aborted rank's stream drains
+        with pytest.raises(me.MEError) as e:
+            eng.gather_device(src, dst)
+        assert e.value.status == me.ME_ECOMM
+        with pytest.raises(me.MEError) as e:
+            eng.comm_check(1000)
+        assert e.value.status == me.ME_ECOMM
+        eng.device_check()
+
+
 def _bench_ranks(nproc, backend, extra=()):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
            f"--nproc-per-node={nproc}", "--master-addr=127.0.0.1", "--master-port=29731",
@@ -124,7 +163,7 @@ def _bench_no_launcher(nproc, backend, extra=()):
     env = {k: v for k, v in os.environ.items()
            if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
     env["OMP_NUM_THREADS"] = "1"
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, env=env)
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=115, env=env)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     lines = r.stdout.splitlines()
     assert len(lines) == 1 and lines[0].startswith("{"), r.stdout
@@ -136,6 +175,11 @@ def _check_stripe_line(d, nproc):
     assert d["config"]["parallelism"] == f"stripe{nproc}"
     assert d["stripe_gather_parity"] is True
     assert d["stripe_4k"]["stripe_gather_parity"] is True
+    # the line verifies its own timed work: gathered fields == batched search
+    # == the committed per-frame pins, every rank's device check clean
+    assert d["parity"] is True, d["parity_legs"]
+    for leg in (d["parity_legs"]["timed_step"], d["stripe_4k"]["parity"]):
+        assert leg["ok"] and leg["pinned_frames"] == leg["pinned_equal"] == leg["frames"], leg
     assert d["stripe_4k"]["parallelism"] == f"stripe{nproc}"
     assert d["value"] > 0 and d["stripe_4k"]["value"] > 0
 
@@ -152,6 +196,16 @@ def test_bench_spawns_its_own_ranks_gloo():
     two ranks, started by bench.py itself, in stripe mode with gather parity
     for the 1080p line and the nested 4K record (gloo: both ranks on one GPU)."""
     _check_stripe_line(_bench_no_launcher(2, "gloo"), 2)
+
+
+@pytest.mark.parametrize("nproc", [4, 8])
+def test_bench_spawns_n_ranks_gloo(nproc):
+    """The SCALE shapes rehearsed on one GPU: `python bench.py --gpus N` (N = 4,
+    8) with no launcher starts N ranks; each searches stripe (r + f) mod N of
+    frame f of the 16-frame step, rank 0 reassembles every frame, and the 1080p
+    and 4K fields equal the batched search and the pins (gloo carries the
+    gather: RCCL needs one GPU per rank)."""
+    _check_stripe_line(_bench_no_launcher(nproc, "gloo", ("--ramp-ms", "10")), nproc)
 
 
 def test_bench_stripe_mode_rccl_one_rank():

@@ -157,3 +157,27 @@ def test_big_cases_pin_frames_and_oracle_band(manifest):
     rec[:, :4] = mv.view(np.uint8).reshape(-1, 4)
     rec[:, 4:] = cost.view(np.uint8).reshape(-1, 4)
     assert hashlib.sha256(rec.tobytes()).hexdigest() == case["band_sha256"][0]
+
+
+def test_bench_pins_agree_with_goldens_and_oracle(manifest):
+    """tests/golden/bench_pins.json (bench.py's per-frame pins of its own timed
+    batches) is tied to the other pins: frame 0 of each SSD batch is the
+    committed reference golden of that synthetic pair, frame 0 of the 4K SAD
+    batch is the whole-frame SAD hash, and a rolled 1080p frame re-searched by
+    the oracle here reproduces its SAD pin."""
+    import bench
+    from motionestimation_amd import synth
+    for cfg, blk, span, golden in (("1080p", 16, 32, "mv/synth1080p_b16_s32.bin"),
+                                   ("4k", 16, 64, "mv/synth4k_b16_s64.bin")):
+        pins = bench.load_pins(cfg, blk, span, "ssd")
+        assert len(pins) == 16
+        raw = open(os.path.join(O.GOLDEN, golden), "rb").read()
+        assert hashlib.sha256(raw).hexdigest() == pins[0], golden
+    big = [c for c in manifest["big_cases"] if c["name"] == "big_4k_b16_s64_sad"][0]
+    assert bench.load_pins("4k", 16, 64, "sad")[0] == big["sha256"]
+    pins = bench.load_pins("1080p", 16, 32, "sad")
+    assert len(pins) == 16
+    ref, cur = bench.batch_frames(*synth.named_pair("1080p"), 6)[5]
+    mv, cost, _ = O.full_search(ref, cur, 16, 32, "sad")
+    rec = bench.record_stream(mv, cost, 1920, 1080, 16, "sad")
+    assert hashlib.sha256(rec).hexdigest() == pins[5]
