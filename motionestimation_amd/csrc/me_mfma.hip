@@ -1516,6 +1516,11 @@ bool launch_mfma_jobs(const SearchArgs& base, const SearchJob* jobs, int n, hipS
   p.cost = jobs[0].cost;
   MfmaGeom g;
   if (jobs[0].r1 <= jobs[0].r0 || !plan_mfma_ssd(p, &g)) return false;
+  // plan_mfma_ssd saw job 0's pointers only: every job's planes must meet the
+  // same alignment (4-byte DMA sources; the block-major kernel's 16-byte cur
+  // row loads), else the batch runs job by job, each planned on its own
+  for (int i = 1; i < n; i++)
+    if ((uintptr_t)jobs[i].ref % 4 || (uintptr_t)jobs[i].cur % (g.bm ? 16 : 4)) return false;
   const size_t stride = batch_stride(g);
   int m = batch_jobs(g, n);
   if (m && (size_t)m * stride > base.scratch_bytes) m = (int)(base.scratch_bytes / stride);

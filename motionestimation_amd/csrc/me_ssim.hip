@@ -44,6 +44,9 @@ constexpr int SSIM_THREADS = 256;
 constexpr int SSIM_Q = 4;   // adjacent candidates per lane (in-kernel statistics)
 constexpr int SSIM_QP = 8;  // ... with the statistics plane (one cross chain each)
 constexpr int SSIM_Q16 = 12; // ... 16 x 16 blocks (1080p +-32: 6: 1.27 ms, 8: 0.88, 12: 0.72, 16: 0.81; profiles/r03bc_*, r03bd_*)
+// LDS bytes past the window: the last row's last candidate group reads up to
+// SSIM_QP (8-candidate groups) or SSIM_Q16 - 1 (16x16 register rows) bytes past it
+constexpr int SSIM_PAD = SSIM_QP > SSIM_Q16 - 1 ? SSIM_QP : SSIM_Q16 - 1;
 
 __device__ __forceinline__ uint64_t wave_min(uint64_t v) {
 #pragma unroll
@@ -262,7 +265,7 @@ __global__ __launch_bounds__(SSIM_THREADS) void me_ssim_kernel(SearchArgs p, int
     const int ngq = (ncx + Q - 1) / Q, ng = ngq * ncy;
     for (int t = tid; t < ng; t += SSIM_THREADS) {
       const int cy = t / ngq, cx0 = (t - cy * ngq) * Q;
-      const uint8_t* r = win + cy * ww + cx0;  // past the window: the launch's padding
+      const uint8_t* r = win + cy * ww + cx0;  // past the window: the launch's SSIM_PAD bytes
       const float2* st = stats + (size_t)(wy0 + cy - pg.ylo) * pg.pitch;
       float fimr[Q], cv[Q];
 #pragma unroll
@@ -421,7 +424,7 @@ hipError_t launch_ssim(const SearchArgs& p, hipStream_t stream) {
   const int B = p.blk;
   long win = (long)(B + 2 * p.range) * (B + 2 * p.range);
   const int cur = (B * B + 15) & ~15;
-  if (cur + win + SSIM_QP > GENERIC_LDS_BUDGET) win = 0;  // read the window from global memory
+  if (cur + win + SSIM_PAD > GENERIC_LDS_BUDGET) win = 0;  // read the window from global memory
   // Patch statistics plane in the context scratch when it holds one (attach_scratch
   // sizes it with ssim_scratch); otherwise every block computes its own.
   SsimPlane sp{0, 0, 0};
@@ -434,9 +437,9 @@ hipError_t launch_ssim(const SearchArgs& p, hipStream_t stream) {
                        dim3(256), 0, stream, p, sp, plane);
     stats = plane;
   }
-  // + SSIM_QP bytes: the last candidate group of the last row reads past the window
+  // + SSIM_PAD bytes: the last candidate group of the last row reads past the window
   hipLaunchKernelGGL(me_ssim_kernel, dim3((unsigned)(rows * p.nbx)), dim3(SSIM_THREADS),
-                     cur + (int)win + SSIM_QP, stream, p, p.block_row_begin, (int)win, stats, sp);
+                     cur + (int)win + SSIM_PAD, stream, p, p.block_row_begin, (int)win, stats, sp);
   return hipGetLastError();
 }
 

@@ -208,6 +208,7 @@ me_status run_pairs(me_ctx* c, Dev& d, const Job& j, int p0, int p1) {
   // ones: at least G + 1 of them.
   const int G = tuning().stream_batch > 0 ? tuning().stream_batch : kPairBatch;
   const size_t cool = (size_t)std::max(cooling_slots(), G + 1);
+  const int flush = tuning().stream_flush >= 0 ? tuning().stream_flush : 0;
   std::vector<SearchJob> jobs;
   jobs.reserve((size_t)G);
   int batch = 0;
@@ -248,6 +249,7 @@ me_status run_pairs(me_ctx* c, Dev& d, const Job& j, int p0, int p1) {
           stage_k ^= 1;
         }
         HIPCHK(c, hipEventRecord(d.slot_ready[si], d.copy));
+        if (flush == 1) (void)hipStreamQuery(d.copy);
         slot_of[f] = si;
       }
       const int sr = slot_of[j.pairs[2 * n]], sc = slot_of[j.pairs[2 * n + 1]];
@@ -259,6 +261,7 @@ me_status run_pairs(me_ctx* c, Dev& d, const Job& j, int p0, int p1) {
                          out_mv + 2 * o, out_cost + o);
       jobs.push_back(SearchJob{d.slots[sr], 0, d.slots[sc], 0, 0, nby, out_mv + 2 * o, out_cost + o});
     }
+    if (flush == 2) (void)hipStreamQuery(d.copy);
     if ((s = me::attach_scratch(c, d, base, false, n1 - n0)) != ME_OK) return s;
     if ((s = me::launch_jobs_ordered(c, d, base, jobs.data(), n1 - n0, d.stream)) != ME_OK) return s;
     if (kAhead <= 8) HIPCHK(c, hipEventRecord(d.pair_ev[batch % kAhead], d.stream));

@@ -21,6 +21,8 @@ struct Tuning {
   int stream_cool = 0;    // ME_STREAM_COOL=1..64: cooling frame slots (0 = automatic)
   int stream_ahead = 0;   // ME_STREAM_AHEAD=1..9: host run-ahead (9: unbounded; 0 = automatic)
   int stream_batch = 0;   // ME_STREAM_BATCH=1..32: pairs per search launch (0 = automatic)
+  int stream_flush = -1;  // ME_STREAM_FLUSH=0..3: how the copy stream's ready markers are pushed
+                          // (0 none, 1 hipStreamQuery after each upload, 2 once per batch; -1 = automatic)
   int flow = -1;          // ME_FLOW=0|1: SAD flow kernel off / allowed (-1 = automatic)
   int flow_slots = 0;     // ME_FLOW_SLOTS=2..16: flow kernel LDS ring slots (0 = automatic)
   int prio = -1;          // ME_PRIO=0|1: staging waves raise their issue priority (-1 = automatic: on)

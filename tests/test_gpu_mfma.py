@@ -239,3 +239,36 @@ def test_mfma_tile_kernel_spans(engine):
                 _check(engine, ref, cur, span, f"tiles {h}x{w} S{span}")
     finally:
         me.set_kernel_path("auto")
+
+
+def test_mfma_batch_mixed_alignment(engine):
+    """A job table of SSD frames whose planes sit at different byte alignments
+    (16, 4, 1 mod 16): the batched matrix-core launch is planned from job 0, so
+    misaligned later jobs must send the batch job by job (each on a kernel its
+    own alignment allows); every job equals the oracle."""
+    import torch
+    w, h, blk, span = 320, 192, 16, 16
+    frames = [synth.frame_pair(w, h, 60 + f, 3 - f, f - 2) for f in range(4)]
+    offs = [0, 4, 1, 16]
+    nb = me.num_blocks(w, h, blk)
+    plane = w * h
+    buf_r = torch.zeros(len(frames) * (plane + 64), dtype=torch.uint8, device="cuda")
+    buf_c = torch.zeros_like(buf_r)
+    jobs, outs = [], []
+    for f, ((r, c), off) in enumerate(zip(frames, offs)):
+        base = f * (plane + 64) + off
+        rt = buf_r[base:base + plane].view(h, w)
+        ct = buf_c[base + (off % 3):base + (off % 3) + plane].view(h, w)
+        rt.copy_(torch.from_numpy(r))
+        ct.copy_(torch.from_numpy(c))
+        mv = torch.full((nb, 2), -9, dtype=torch.int16, device="cuda")
+        co = torch.zeros(nb, dtype=torch.int32, device="cuda")
+        jobs.append((rt, 0, ct, 0, 0, (h + blk - 1) // blk, mv, co))
+        outs.append((mv, co))
+    engine.search_stripes_device(w, h, blk, span, "ssd", jobs, stride=w)
+    torch.cuda.synchronize()
+    engine.device_check()
+    for f, ((r, c), (mv, co)) in enumerate(zip(frames, outs)):
+        omv, oco, _ = O.full_search(r, c, blk, span, "ssd", threads=NT)
+        np.testing.assert_array_equal(mv.cpu().numpy(), omv, err_msg=f"job {f}")
+        np.testing.assert_array_equal(co.cpu().numpy().view(np.uint32), oco, err_msg=f"job {f}")
