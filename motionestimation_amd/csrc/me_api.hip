@@ -63,7 +63,8 @@ static Tuning read_tuning() {
   env_int("ME_STREAM_COOL", 1, 64, &t.stream_cool);
   env_int("ME_STREAM_AHEAD", 1, 9, &t.stream_ahead);
   env_int("ME_STREAM_BATCH", 1, 32, &t.stream_batch);
-  env_int("ME_STREAM_FLUSH", 0, 3, &t.stream_flush);
+  env_int("ME_STREAM_FLUSH", 0, 4, &t.stream_flush);
+  env_int("ME_STREAM_FENCE", 0, 2, &t.stream_fence);
   env_int("ME_FLOW", 0, 1, &t.flow);
   env_int("ME_FLOW_SLOTS", 2, 16, &t.flow_slots);
   env_int("ME_PRIO", 0, 1, &t.prio);
@@ -71,6 +72,7 @@ static Tuning read_tuning() {
   env_int("ME_FAIR", 0, 3, &t.fair);
   env_int("ME_FLOW_ONE", 0, 1, &t.flow_one);
   env_int("ME_MFMA_BATCH", 0, 1, &t.mfma_batch);
+  env_int("ME_MFMA_S2K", 0, 1, &t.mfma_s2k);
   if (const char* e = getenv("ME_FAIR_T")) {
     int lo = 0, hi = 0;
     if (sscanf(e, "%d,%d", &lo, &hi) == 2 && lo >= 1 && lo <= hi && hi <= 255) {

@@ -59,6 +59,8 @@ struct Dev {
   hipEvent_t pair_ev[8] = {};  // search of pair n done: bounds how far the host runs ahead
   uint8_t* pair_out = nullptr;  // [pairs][nblocks] mv records, then [pairs][nblocks] costs
   size_t pair_out_cap = 0;
+  uint8_t* tick_h = nullptr;     // 64 pinned bytes: the copy stream's trailing tick copy
+  uint8_t* tick_d = nullptr;     //   (me_stream.hip) and its device target
   // An invariant report that a synchronous entry point read (and cleared on
   // the device) on behalf of earlier asynchronous searches: me_device_check
   // still reports it once (device_status sets it, me_device_check clears it).

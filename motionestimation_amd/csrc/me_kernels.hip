@@ -1973,7 +1973,8 @@ hipError_t launch_jobs(const SearchArgs& base, const SearchJob* jobs, int n, hip
   // per job in the context scratch); others go one by one
   if (n > 1 && launch_mfma_jobs(base, jobs, n, stream, &e)) return e;
   MfmaGeom mg;
-  const bool mfma = base.cost_kind == COST_SSD && base.scratch && plan_mfma_ssd(job_args(base, jobs[0]), &mg);
+  const bool mfma = base.cost_kind == COST_SSD && plan_mfma_ssd(job_args(base, jobs[0]), &mg) &&
+                    (mg.bmv || base.scratch);
   if (n > 1 && !mfma && launch_item_jobs(base, jobs, n, stream, &e)) return e;
   for (int i = 0; i < n; i++) {
     if (jobs[i].r1 <= jobs[i].r0) continue;
@@ -1989,8 +1990,8 @@ hipError_t launch_search(const SearchArgs& p, hipStream_t stream, int* used_fast
   if (used_fast) *used_fast = 0;
   if (p.cost_kind == COST_SSIM) return launch_ssim(p, stream);
   MfmaGeom mg;
-  if (p.cost_kind == COST_SSD && p.scratch && plan_mfma_ssd(p, &mg) &&
-      p.scratch_bytes >= mg.scratch_bytes) {
+  if (p.cost_kind == COST_SSD && plan_mfma_ssd(p, &mg) &&
+      (mg.bmv || (p.scratch && p.scratch_bytes >= mg.scratch_bytes))) {
     // Matrix cores: every full-width block (the partial bottom row included);
     // the partial right column stays on the generic kernel.
     hipError_t e = launch_mfma_ssd(p, mg, stream);

@@ -1252,6 +1252,415 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_bm16_kernel(SearchArgs p, M
   }
 }
 
+// --------------------------- 16x16, block-major, S2 formed in the workgroup
+// me_mfma_bmv_kernel: the block-major kernel above without the prepass and its
+// HBM planes (the rp bytes and the 4-byte S2 plane were 7.5x the algorithmic
+// bytes of a 1080p search, DESIGN.md "SSD-path HBM traffic").  The band window
+// is DMA'd from the reference plane itself, and every band's S2 is formed in
+// LDS from the window the band already holds:
+//   phase A  lane = position p: H(row, p) = sum_{4 bytes} (r^2 - 254 r), two
+//            v_dot4 per row; V(k, p) = sum_{i < hb} H(k + i, p) by a sliding
+//            sum down the 15 + hb window rows (raw bytes: it runs before the
+//            window is XOR-ed)
+//   phase B  S2(k, x) = V(k, x) + V(k, x + 4) + V(k, x + 8) + V(k, x + 12)
+//            (+ 256 * 127^2, folded into the key constant), in place
+//   the window's bytes are XOR-ed with 0x80 (r' = r - 128, the B operand)
+// The tiles then read S2 from LDS instead of the plane.  crec (the cur row
+// records) aliases the S2 plane: the A fragments are built before band 0.
+// S <= 64 (window pitch 288): LDS 35 KB, four workgroups per CU as before.
+constexpr int BMV_NP = 268;                // S2 / V plane row pitch (ints): 256 positions + 12 V; 67 * 4
+constexpr int BMV_PLANE = 16 * BMV_NP * 4; // 17,152 bytes (>= the 6,144 of crec)
+constexpr int BMV_KEYS = 8 * 8 + 8 * 4;    // keys, cc
+constexpr int BMV_LP = 288;
+constexpr int BMV_LDS = BMV_KEYS + BMV_PLANE + 2 * 31 * BMV_LP;
+static_assert(8 * 16 * BM_CREC <= BMV_PLANE, "crec aliases the S2 plane");
+constexpr int BMV_S2C = 256 * 127 * 127;   // the constant part of S2 = sum (r - 127)^2
+
+// r^2 - 254 r summed over the 4 bytes of v (S2 = sum of these + 256 * 127^2)
+__device__ __forceinline__ int h4(uint32_t v) {
+  return (int)__builtin_amdgcn_udot4(v, v, 0u, false) -
+         (int)__builtin_amdgcn_udot4(v, 0xFEFEFEFEu, 0u, false);
+}
+
+// Phase A, 16-row blocks: V(k, p) for the 16 band rows k, position p (window
+// column p), from window rows 0..30 (raw bytes, pitch LP); written to vcol[k * BMV_NP].
+template <int LP>
+__device__ __forceinline__ void bmv_vsum16(const uint8_t* win, int p, int* vcol) {
+  typedef __attribute__((address_space(3))) const uint32_t lds_c32;
+  const uint32_t a = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) const uint8_t*)win) +
+                     (uint32_t)(p & ~3);
+  const uint32_t sh = (uint32_t)(p & 3);
+  auto row = [&](int k) {
+    const uint32_t d0 = *reinterpret_cast<lds_c32*>((uintptr_t)(a + (uint32_t)(k * LP)));
+    const uint32_t d1 = *reinterpret_cast<lds_c32*>((uintptr_t)(a + (uint32_t)(k * LP) + 4u));
+    return __builtin_amdgcn_alignbyte(d1, d0, sh);
+  };
+  // The column's own plane entries hold H(k) until V(k) replaces them (no
+  // register array: the A fragments keep 64 VGPRs live across this phase).
+  int v = 0;
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    const int hk = h4(row(k));
+    vcol[k * BMV_NP] = hk;
+    v += hk;
+  }
+#pragma unroll
+  for (int k = 1; k < 16; k++) {
+    const int old = vcol[(k - 1) * BMV_NP];
+    vcol[(k - 1) * BMV_NP] = v;
+    v += h4(row(k + 15)) - old;
+  }
+  vcol[15 * BMV_NP] = v;
+}
+
+// Phase A for a partial bottom block row (block height hb < 16): direct sums.
+// S2 there has hb * 16 * 127^2 as its constant, not the 256 * 127^2 the key
+// constant holds: each of the four V terms of an S2 carries a quarter of the difference.
+template <int LP>
+__device__ __forceinline__ void bmv_vsum_hb(const uint8_t* win, int p, int hb, int* vcol) {
+  typedef __attribute__((address_space(3))) const uint32_t lds_c32;
+  const uint32_t a = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) const uint8_t*)win) +
+                     (uint32_t)(p & ~3);
+  const uint32_t sh = (uint32_t)(p & 3);
+  for (int k = 0; k < 16; k++) {
+    int v = -(16 - hb) * 4 * 127 * 127;
+    for (int i = 0; i < hb; i++) {
+      const uint32_t o = a + (uint32_t)((k + i) * LP);
+      v += h4(__builtin_amdgcn_alignbyte(*reinterpret_cast<lds_c32*>((uintptr_t)(o + 4u)),
+                                         *reinterpret_cast<lds_c32*>((uintptr_t)o), sh));
+    }
+    vcol[k * BMV_NP] = v;
+  }
+}
+
+__global__ __launch_bounds__(256)
+__attribute__((amdgpu_waves_per_eu(4))) void me_mfma_bmv_kernel(SearchArgs p, MfmaGeom g, MfmaJobs jb) {
+  constexpr int LP = BMV_LP;
+  constexpr int WINB = 31 * LP;  // one band's window rows
+  extern __shared__ __align__(16) uint8_t smem[];
+  unsigned long long* keys = reinterpret_cast<unsigned long long*>(smem);
+  int* cc = reinterpret_cast<int*>(smem + 64);
+  int* plane = reinterpret_cast<int*>(smem + BMV_KEYS);  // S2 (phase B) / V (phase A), [16][BMV_NP]
+  uint8_t* crec = smem + BMV_KEYS;                       // until the A fragments are built
+  uint8_t* win = smem + BMV_KEYS + BMV_PLANE;
+
+  const int tid = (int)threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int n = lane & 15, h = lane >> 4;
+  const int S = p.range, W = p.width, H = p.height;
+  int lin;
+  {  // XCD-banded: XCD x walks one contiguous run of strips
+    const int nwg = (int)gridDim.x, bid = (int)blockIdx.x;
+    const int x = bid & 7, m = bid >> 3, q = nwg >> 3, rem = nwg & 7;
+    lin = x * q + min(x, rem) + m;
+  }
+  {  // batched launch: jobs are consecutive runs of jb.wgs workgroups
+    const int j = lin / jb.wgs;
+    lin -= j * jb.wgs;
+    mfma_job(jb, j, p, g);
+  }
+  const int brl = lin / g.bm_wpr, sx = lin - brl * g.bm_wpr;
+  const int br = g.row0 + brl;
+  const int bc0 = 8 * sx, nb = min(8, g.nbx - bc0);
+  const int by = 16 * br, bh = br == g.hb_row ? g.hb : 16;
+  const int ylo = max(by - S, 0), yhi = min(by + S, H - bh);
+  const int Ty = (yhi - ylo + 16) >> 4;
+  const int tc0 = max(16 * bc0 - S, 0) >> 4;
+  // positions the workgroup's tiles read: 16 (tile of the last block's x range
+  // end - tc0 + 1); V is needed 12 positions further
+  const int npos = 16 * ((min(16 * (bc0 + nb - 1) + S, W - 16) >> 4) - tc0 + 1);
+  const int npv = npos + 12;
+  const bool yover = yhi - ylo >= 15;
+  auto band_y = [&](int s) { return yover ? min(ylo + 16 * s, yhi - 15) : ylo + 16 * s; };
+  // band window: frame rows [Ys, Ys + 31) x columns [16 tc0, 16 tc0 + LP) of the
+  // reference plane (rows past the resident ones read as zeros: masked), double-buffered
+  const __amdgpu_buffer_rsrc_t rref =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.ref, (short)0, p.ref_bytes, 0x00020000);
+  auto stage_band = [&](int s) {
+    const int gbase = (band_y(s) - p.ref_row0) * p.stride + 16 * tc0;
+    dma16(rref, win + (s & 1) * WINB, WINB, [&](int d) {
+      const int rho = d / LP, k = d - rho * LP;
+      return (uint32_t)(gbase + rho * p.stride + k);
+    });
+  };
+  // S2 of band s (its window has landed in buffer s & 1; everyone is past the
+  // previous band's tiles): V, then S2 in place, and the window XOR-ed for the MFMAs.
+  auto band_s2 = [&](int s) {
+    uint8_t* wb = win + (s & 1) * WINB;
+#pragma unroll 1
+    for (int pp = tid; pp < npv; pp += 256) {
+      if (bh == 16) bmv_vsum16<LP>(wb, pp, plane + pp);
+      else bmv_vsum_hb<LP>(wb, pp, bh, plane + pp);
+    }
+    __syncthreads();
+    typedef int i32x4 __attribute__((ext_vector_type(4)));
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    constexpr int QB = 64;       // 4-position groups per plane row (256 positions)
+    i32x4 o[4];
+    const int nq = npos >> 2;
+#pragma unroll
+    for (int t = 0; t < 4; t++) {  // 16 rows x 64 groups = 1,024 tasks, 4 per lane
+      const int task = tid + 256 * t, k = task / QB, q = task - k * QB;
+      if (q < nq) {
+        const i32x4* vr = reinterpret_cast<const i32x4*>(plane + k * BMV_NP + 4 * q);
+        const i32x4 v0 = vr[0], v1 = vr[1], v2 = vr[2], v3 = vr[3];
+        o[t] = v0 + v1 + v2 + v3;
+      }
+    }
+    // the window's bytes become r' = r ^ 0x80 (the MFMA B operand)
+    for (int d = tid; d < WINB / 16; d += 256) {
+      u32x4* w4 = reinterpret_cast<u32x4*>(wb) + d;
+      *w4 = *w4 ^ 0x80808080u;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+      const int task = tid + 256 * t, k = task / QB, q = task - k * QB;
+      if (q < nq) *reinterpret_cast<i32x4*>(plane + k * BMV_NP + 4 * q) = o[t];
+    }
+    __syncthreads();
+  };
+
+  MS_STAMP(0, __builtin_amdgcn_s_memtime());
+  MS_STAMP(6, __builtin_amdgcn_s_memrealtime());
+  if (tid < 8) {
+    keys[tid] = ~0ull;
+    cc[tid] = 0;
+  }
+  stage_band(0);
+  __syncthreads();  // keys / cc initialised
+  if (tid < 128) {  // cur row records (c ^ 0x7F) and Cc = sum(c''^2 + 2 c'')
+    const int j = tid >> 4, rho = tid & 15;
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if (j < nb && rho < bh) {
+      const u32x4* src = reinterpret_cast<const u32x4*>(
+          p.cur + (ptrdiff_t)(by + rho - p.cur_row0) * p.stride + 16 * (bc0 + j));
+      v = *src ^ 0x7F7F7F7Fu;
+    }
+    const u32x4 z = {0u, 0u, 0u, 0u};
+    u32x4* rec = reinterpret_cast<u32x4*>(crec + (16 * j + rho) * BM_CREC);
+    rec[0] = z;
+    rec[1] = v;
+    rec[2] = z;
+    int part = 0;
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+      part = __builtin_amdgcn_sdot4((int)v[e], (int)v[e], part, false);
+      part = __builtin_amdgcn_sdot4((int)v[e], 0x02020202, part, false);
+    }
+    if (j < nb) atomicAdd(&cc[j], part);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  const int j0 = 2 * wave, j1 = j0 + 1;
+  const bool hasA = j0 < nb, hasB = j1 < nb;
+  const int bxA = 16 * (bc0 + j0), bxB = bxA + 16;
+  const int xloA = max(bxA - S, 0), xhiA = min(bxA + S, W - 16);
+  const int xloB = max(bxB - S, 0), xhiB = min(bxB + S, W - 16);
+  const int i0A = xloA >> 4, i1A = xhiA >> 4, i0B = xloB >> 4, i1B = xhiB >> 4;
+  const int iu0 = i0A, iu1 = hasB ? i1B : i1A;
+
+  v4i aA[8], aB[8];
+  {
+    const int o = 16 + 16 * (h & 1) - n, sh = o & 3;
+    typedef __attribute__((address_space(3))) const uint32_t lds_c32;
+    const uint32_t lb = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) uint8_t*)crec) +
+                        (uint32_t)((h >> 1) * BM_CREC + (o & ~3));
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+#pragma unroll
+      for (int bsel = 0; bsel < 2; bsel++) {
+        const uint32_t a0 = lb + (uint32_t)(((2 * wave + bsel) * 16 + 2 * q) * BM_CREC);
+        uint32_t d[5];
+#pragma unroll
+        for (int e = 0; e < 5; e++) d[e] = *reinterpret_cast<lds_c32*>((uintptr_t)(a0 + 4 * e));
+        v4i f;
+#pragma unroll
+        for (int e = 0; e < 4; e++) f[e] = (int)__builtin_amdgcn_alignbyte(d[e + 1], d[e], sh);
+        if (bsel == 0) aA[q] = f; else aB[q] = f;
+      }
+    }
+  }
+  MS_STAMP(1, __builtin_amdgcn_s_memtime());
+  __syncthreads();  // crec read by every wave: the plane is free for band 0's S2
+  band_s2(0);
+  uint32_t mbits = 0;
+  {
+    auto xmask = [&](int e, int i, int xlo, int xhi) {
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int x = 16 * i + 4 * h + r;
+        if (x < xlo || x > xhi) mbits |= 1u << (4 * e + r);
+      }
+    };
+    xmask(0, i0A, xloA, xhiA);
+    xmask(1, i1A, xloA, xhiA);
+    xmask(2, i0B, xloB, xhiB);
+    xmask(3, i1B, xloB, xhiB);
+  }
+  const uint32_t ym = (!yover && n > yhi - ylo) ? 0x80000000u : 0u;
+  const bool fast = hasB && yover && bxA - S >= 0 && bxB + S <= W - 16 && i1A - i0A >= 2;
+  const int mfa = (bxA - S) & 15, mlb = (bxA + S) & 15;
+  // S2 of lane (n, h) at tile i: plane row n, positions 16 (i - tc0) + 4 h ..
+  const uint32_t s2base = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) int*)plane) +
+                          (uint32_t)((n * BMV_NP + 4 * h - 16 * tc0) * 4);
+  const uint32_t lbase = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) uint8_t*)win) +
+                         (uint32_t)((n + (h >> 1)) * LP + 16 * (h & 1) - 16 * tc0);
+  typedef __attribute__((address_space(3))) const v4i lds_v4i;
+  const v4i zero4 = {0, 0, 0, 0};
+
+  unsigned long long bestA = ~0ull, bestB = ~0ull;
+  for (int s = 0; s < Ty; s++) {
+    if (s + 1 < Ty) stage_band(s + 1);
+    if (hasA) {
+      const uint32_t lrow0 = lbase + (uint32_t)((s & 1) * WINB);
+      uint32_t bA = ~0u, bB = ~0u;
+      // first / last tile masks, formed per band (not held across band_s2:
+      // opaque keeps the compiler from hoisting them out of the band loop)
+      v4i mF, mL;
+      const int h4b = opaque(4 * h);
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int m = h4b + r;
+        mF[r] = m < mfa ? (1 << 24) : 0;
+        mL[r] = m > mlb ? (1 << 24) : 0;
+      }
+      auto widen = [&](int seg) {
+        const uint32_t lo = ((uint32_t)s << 8) | ((uint32_t)seg << 6);
+        const unsigned long long kA = ((unsigned long long)(bA >> 6) << 32) | lo | (bA & 63u);
+        const unsigned long long kB = ((unsigned long long)(bB >> 6) << 32) | lo | (bB & 63u);
+        bestA = (kA >> 32) < (bestA >> 32) ? kA : bestA;
+        bestB = (kB >> 32) < (bestB >> 32) ? kB : bestB;
+        bA = ~0u;
+        bB = ~0u;
+      };
+      auto tile = [&](int i, auto DA, auto DB, auto MA, auto MB) {
+        constexpr bool da = decltype(DA)::value, db = decltype(DB)::value;
+        constexpr int ma = decltype(MA)::value, mb = decltype(MB)::value;
+        const v4i s2c = *reinterpret_cast<lds_v4i*>((uintptr_t)(s2base + (uint32_t)(64 * i)));
+        const uint32_t lrow = (uint32_t)opaque((int)(lrow0 + (uint32_t)(16 * i)));
+        v4i accA = ma == 1 ? mF : ma == 2 ? mL : zero4;
+        v4i accB = mb == 1 ? mF : mb == 2 ? mL : zero4;
+        auto ld = [&](int q) {
+          return *reinterpret_cast<lds_v4i*>((uintptr_t)(lrow + (uint32_t)(2 * q * LP)));
+        };
+        v4i f0 = ld(0), f1 = ld(1);
+#pragma unroll
+        for (int qp = 0; qp < 4; qp++) {
+          v4i n0 = f0, n1 = f1;
+          if (qp < 3) {
+            n0 = ld(2 * qp + 2);
+            n1 = ld(2 * qp + 3);
+          }
+          if constexpr (da) accA = MFMA16(aA[2 * qp], f0, accA, 0, 0, 0);
+          if constexpr (db) accB = MFMA16(aB[2 * qp], f0, accB, 0, 0, 0);
+          if constexpr (da) accA = MFMA16(aA[2 * qp + 1], f1, accA, 0, 0, 0);
+          if constexpr (db) accB = MFMA16(aB[2 * qp + 1], f1, accB, 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
+          f0 = n0;
+          f1 = n1;
+        }
+        // key = ((2 acc + S2 + 1 + 2^23) << 6) + 4 ((i - iu0) & 15) + r with
+        // S2 = s2c + 256 * 127^2 (the constant in kb)
+        const int rel = i - iu0;
+        const uint32_t kb = (1u << 29) + 64u + ((uint32_t)BMV_S2C << 6) + 4u * (uint32_t)(rel & 15);
+        uint32_t P[4];
+#pragma unroll
+        for (int r = 0; r < 4; r++) P[r] = lshl6_add((uint32_t)s2c[r], kb + (uint32_t)r);
+        auto keys_of = [&](v4i acc, uint32_t& best, int i0, int i1, int e0, auto GEN) {
+          if constexpr (decltype(GEN)::value) {
+            if (i == i0 || i == i1) {
+              const int e = i == i0 ? e0 : e0 + 1;
+              const uint32_t mb4 = (uint32_t)opaque((int)mbits);
+#pragma unroll
+              for (int r = 0; r < 4; r++)
+                acc[r] += (int)(__builtin_amdgcn_ubfe(mb4, (uint32_t)(4 * e + r), 1u) << 24);
+            }
+          }
+          uint32_t k[4];
+#pragma unroll
+          for (int r = 0; r < 4; r++) k[r] = ((uint32_t)acc[r] << 7) + P[r];
+          if constexpr (decltype(GEN)::value) {
+#pragma unroll
+            for (int r = 0; r < 4; r++) k[r] |= ym;
+          }
+          best = umin3(best, k[0], k[1]);
+          best = umin3(best, k[2], k[3]);
+        };
+        if constexpr (da) keys_of(accA, bA, i0A, i1A, 0, std::integral_constant<bool, ma == 3>{});
+        if constexpr (db) keys_of(accB, bB, i0B, i1B, 2, std::integral_constant<bool, mb == 3>{});
+        if ((rel & 15) == 15 && i < iu1) widen(rel >> 4);
+      };
+      using T_ = std::true_type;
+      using F_ = std::false_type;
+      using M0 = std::integral_constant<int, 0>;
+      using M1 = std::integral_constant<int, 1>;
+      using M2 = std::integral_constant<int, 2>;
+      using M3 = std::integral_constant<int, 3>;
+      if (fast) {
+        tile(i0A, T_{}, F_{}, M1{}, M0{});
+        tile(i0A + 1, T_{}, T_{}, M0{}, M1{});
+        for (int i = i0A + 2; i < i1A; i++) tile(i, T_{}, T_{}, M0{}, M0{});
+        tile(i1A, T_{}, T_{}, M2{}, M0{});
+        tile(i1B, F_{}, T_{}, M0{}, M2{});
+      } else {
+        for (int i = iu0; i <= iu1; i++) {
+          const bool useA = i <= i1A, useB = hasB && i >= i0B;
+          if (useA && useB) tile(i, T_{}, T_{}, M3{}, M3{});
+          else if (useA) tile(i, T_{}, F_{}, M3{}, M3{});
+          else tile(i, F_{}, T_{}, M3{}, M3{});
+        }
+      }
+      widen((iu1 - iu0) >> 4);
+    }
+    if (s == 0) MS_STAMP(2, __builtin_amdgcn_s_memtime());
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // band s + 1 landed (this thread's pieces)
+    __syncthreads();                                   // ... and everyone's; band s and its S2 free
+    if (s + 1 < Ty) band_s2(s + 1);
+  }
+  if (hasA) {
+    auto emit = [&](unsigned long long b, int j, int ccj, int bx) {
+      const uint32_t hi = (uint32_t)(b >> 32);
+      if (hi < (1u << 25)) {
+        const uint32_t lo = (uint32_t)b;
+        const int sb = (int)(lo >> 8), seg = (int)((lo >> 6) & 3u), idx = (int)(lo & 63u);
+        const uint32_t cost = hi - 1u - (1u << 23) + (uint32_t)ccj;
+        const int dx = 16 * (iu0 + 16 * seg + (idx >> 2)) + 4 * h + (idx & 3) - bx;
+        const int dy = band_y(sb) + n - by;
+        const unsigned long long key = ((unsigned long long)cost << 32) |
+                                       ((uint32_t)(dy + 32768) << 16) | (uint32_t)(dx + 32768);
+        const uint32_t a = (uint32_t)(uintptr_t)(
+            (__attribute__((address_space(3))) unsigned long long*)(keys + j));
+        asm volatile("ds_min_u64 %0, %1" : : "v"(a), "v"(key) : "memory");
+      }
+    };
+    emit(bestA, j0, cc[j0], bxA);
+    if (hasB) emit(bestB, j1, cc[j1], bxB);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+#ifdef ME_STAMPS
+  if (tid == 0 && blockIdx.x < (1u << 14)) {
+    unsigned hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    g_mstamps[8 * blockIdx.x + 3] = __builtin_amdgcn_s_memtime();
+    g_mstamps[8 * blockIdx.x + 4] = hw;
+    g_mstamps[8 * blockIdx.x + 5] = xcc;
+    g_mstamps[8 * blockIdx.x + 7] = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
+  if (tid < nb) {
+    const unsigned long long kk = keys[tid];
+    const int out = (br - p.block_row_begin) * p.nbx + bc0 + tid;
+    p.mv[2 * out] = (int16_t)((int)(kk & 0xFFFF) - 32768);
+    p.mv[2 * out + 1] = (int16_t)((int)((kk >> 16) & 0xFFFF) - 32768);
+    if (p.cost) p.cost[out] = (uint32_t)(kk >> 32);
+  }
+}
+
 }  // namespace
 
 // Process-wide path switch (me_set_kernel_path / ME_PATH, me_tuning.h).
@@ -1332,6 +1741,10 @@ bool plan_mfma_ssd(const SearchArgs& p, MfmaGeom* g) {
   g->lds = 4 * (L + 15) * (64 * g->ngxw + 32) + 16 * 8 + 16 * 4 + L * 256 * g->ngxw;
   g->bm_wpr = (g->nbx + 7) / 8;
   if (g->bm) g->lds = BM_HDR + 2 * 31 * g->bm_lp;
+  // S <= 64 (window pitch 288): S2 formed in the workgroup, no prepass planes
+  // (ME_MFMA_S2K=0: the prepass kernel; tuning build)
+  g->bmv = g->bm && g->bm_lp == BMV_LP && tuning().mfma_s2k != 0;
+  if (g->bmv) g->lds = BMV_LDS;
   g->mkeys = p.mkeys;
   g->mcnt = p.mcnt;
   g->ya0 = max(r0 * 16 - S, 0);
@@ -1359,6 +1772,11 @@ bool plan_mfma_ssd(const SearchArgs& p, MfmaGeom* g) {
   g->rp = reinterpret_cast<int8_t*>(p.scratch);
   g->s2 = p.scratch ? reinterpret_cast<int*>(p.scratch + rp_alloc) : nullptr;
   g->s2h = p.scratch ? reinterpret_cast<int*>(p.scratch + rp_alloc + s2_plane) : nullptr;
+  if (g->bmv) {  // no planes: the kernel reads the reference plane
+    g->scratch_bytes = 0;
+    g->rp = nullptr;
+    g->s2 = g->s2h = nullptr;
+  }
   return true;
 }
 
@@ -1380,6 +1798,7 @@ static bool plan_mfma_ssd8(const SearchArgs& p, MfmaGeom* g) {
   g->hb = 8;
   g->hb_row = -1;
   g->bm = 0;
+  g->bmv = 0;
   g->nbx = W / 8;
   g->tiles_x = (g->nbx + 3) / 4;
   g->tiles_y = (g->nrows + 3) / 4;
@@ -1447,8 +1866,16 @@ static hipError_t launch_bm16(const SearchArgs& p, const MfmaGeom& g, const Mfma
   return hipGetLastError();
 }
 
+static hipError_t launch_bmv(const SearchArgs& p, const MfmaGeom& g, const MfmaJobs& jb,
+                             hipStream_t stream) {
+  hipLaunchKernelGGL(me_mfma_bmv_kernel, dim3((unsigned)(jb.n * jb.wgs)), dim3(256), g.lds, stream,
+                     p, g, jb);
+  return hipGetLastError();
+}
+
 hipError_t launch_mfma_ssd(const SearchArgs& p, const MfmaGeom& g, hipStream_t stream) {
   const MfmaJobs jb = single_job(p, g);
+  if (g.bmv) return launch_bmv(p, g, jb, stream);
   hipError_t e = launch_prep(p, g, jb, stream);
   if (e != hipSuccess) return e;
   if (p.blk == 8) {
@@ -1485,6 +1912,7 @@ static size_t batch_stride(const MfmaGeom& g) { return (g.scratch_bytes + 255) &
 // apply (not the block-major kernel, or one job's planes alone exceed the cap).
 static int batch_jobs(const MfmaGeom& g, int n) {
   if (!g.bm || n < 2) return 0;
+  if (g.bmv) return n < MAX_JOBS ? n : MAX_JOBS;  // no prepass planes
   const size_t per = MFMA_BATCH_SCRATCH / batch_stride(g);
   const int m = (int)(per < (size_t)MAX_JOBS ? per : (size_t)MAX_JOBS);
   return m >= 2 ? (n < m ? n : m) : 0;
@@ -1492,7 +1920,7 @@ static int batch_jobs(const MfmaGeom& g, int n) {
 
 size_t mfma_batch_scratch(const SearchArgs& p, int n) {
   MfmaGeom g;
-  if (!plan_mfma_ssd(p, &g)) return 0;
+  if (!plan_mfma_ssd(p, &g) || g.bmv) return 0;
   const int m = batch_jobs(g, n);
   return m ? (size_t)m * batch_stride(g) : g.scratch_bytes;
 }
@@ -1500,7 +1928,7 @@ size_t mfma_batch_scratch(const SearchArgs& p, int n) {
 bool launch_mfma_jobs(const SearchArgs& base, const SearchJob* jobs, int n, hipStream_t stream,
                       hipError_t* err) {
   *err = hipSuccess;
-  if (base.cost_kind != COST_SSD || n < 2 || !base.scratch || tuning().mfma_batch == 0) return false;
+  if (base.cost_kind != COST_SSD || n < 2 || tuning().mfma_batch == 0) return false;
   for (int i = 1; i < n; i++)  // one geometry: the same rows of same-sized frames
     if (jobs[i].r0 != jobs[0].r0 || jobs[i].r1 != jobs[0].r1 ||
         jobs[i].ref_row0 != jobs[0].ref_row0 || jobs[i].cur_row0 != jobs[0].cur_row0)
@@ -1521,9 +1949,10 @@ bool launch_mfma_jobs(const SearchArgs& base, const SearchJob* jobs, int n, hipS
   // row loads), else the batch runs job by job, each planned on its own
   for (int i = 1; i < n; i++)
     if ((uintptr_t)jobs[i].ref % 4 || (uintptr_t)jobs[i].cur % (g.bm ? 16 : 4)) return false;
-  const size_t stride = batch_stride(g);
+  const size_t stride = g.bmv ? 0 : batch_stride(g);
   int m = batch_jobs(g, n);
-  if (m && (size_t)m * stride > base.scratch_bytes) m = (int)(base.scratch_bytes / stride);
+  if (!g.bmv && (!base.scratch || (m && (size_t)m * stride > base.scratch_bytes)))
+    m = base.scratch ? (int)(base.scratch_bytes / stride) : 0;
   if (m < 2 || g.nbx < p.nbx) return false;  // (a partial right column: job by job)
   for (int i0 = 0; i0 < n && *err == hipSuccess; i0 += m) {
     MfmaJobs jb;
@@ -1537,8 +1966,12 @@ bool launch_mfma_jobs(const SearchArgs& base, const SearchJob* jobs, int n, hipS
       jb.mv[j] = J.mv;
       jb.cost[j] = J.cost;
     }
-    *err = launch_prep(p, g, jb, stream);
-    if (*err == hipSuccess) *err = launch_bm16(p, g, jb, stream);
+    if (g.bmv) {
+      *err = launch_bmv(p, g, jb, stream);
+    } else {
+      *err = launch_prep(p, g, jb, stream);
+      if (*err == hipSuccess) *err = launch_bm16(p, g, jb, stream);
+    }
   }
   return true;
 }

@@ -43,6 +43,14 @@ std::map<uintptr_t, size_t> g_pinned;  // me_host_alloc ranges: base -> bytes
 static int cooling_slots() { return tuning().stream_cool > 0 ? tuning().stream_cool : 2; }
 // Pairs per search launch (ME_STREAM_BATCH overrides; tuning)
 constexpr int kPairBatch = 4;
+// Flags of the pipeline's ordering events (slot ready / slot free / pair done):
+// they order work of this device's own streams (and bound the host's run-ahead),
+// so a device-scope release is enough (ME_STREAM_FENCE overrides; tuning)
+unsigned pipe_event_flags() {
+  const int f = tuning().stream_fence >= 0 ? tuning().stream_fence : 0;
+  return hipEventDisableTiming |
+         (f == 1 ? hipEventDisableSystemFence : f == 2 ? hipEventReleaseToDevice : 0u);
+}
 }  // namespace
 
 bool host_range_pinned(const void* p, size_t bytes) {
@@ -79,6 +87,9 @@ void release_pipeline(Dev& d) {
   (void)hipFree(d.pair_out);
   d.pair_out = nullptr;
   d.pair_out_cap = 0;
+  if (d.tick_h) (void)hipHostFree(d.tick_h);
+  (void)hipFree(d.tick_d);
+  d.tick_h = d.tick_d = nullptr;
   if (d.copy) (void)hipStreamDestroy(d.copy);
   d.copy = nullptr;
 }
@@ -130,8 +141,8 @@ me_status new_slot(me_ctx* c, Dev& d, int* idx) {
   if (hipMalloc((void**)&p, d.slot_bytes) != hipSuccess)
     return fail(c, ME_ENOMEM, "hipMalloc(%zu) for a frame slot failed", d.slot_bytes);
   hipEvent_t r = nullptr, f = nullptr;
-  if (hipEventCreateWithFlags(&r, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&f, hipEventDisableTiming) != hipSuccess) {
+  if (hipEventCreateWithFlags(&r, pipe_event_flags()) != hipSuccess ||
+      hipEventCreateWithFlags(&f, pipe_event_flags()) != hipSuccess) {
     (void)hipFree(p);
     if (r) (void)hipEventDestroy(r);
     return fail(c, ME_EDEVICE, "hipEventCreate failed");
@@ -200,7 +211,7 @@ me_status run_pairs(me_ctx* c, Dev& d, const Job& j, int p0, int p1) {
   const int env_ahead = tuning().stream_ahead;  // tuning build: 1..8, 9 unbounded (diagnostic)
   const int kAhead = env_ahead > 8 ? 1 << 30 : env_ahead >= 1 ? env_ahead : (all_pinned ? 2 : 3);
   for (auto& e : d.pair_ev)
-    if (!e) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    if (!e) HIPCHK(c, hipEventCreateWithFlags(&e, pipe_event_flags()));
   // Pairs are searched G at a time in one job-table launch (launch_jobs: the
   // flow / item kernels' job tables, SSD pairs sharing the matrix cores'
   // launches), so a launch's fill and drain are paid once per G pairs.  The
@@ -209,6 +220,10 @@ me_status run_pairs(me_ctx* c, Dev& d, const Job& j, int p0, int p1) {
   const int G = tuning().stream_batch > 0 ? tuning().stream_batch : kPairBatch;
   const size_t cool = (size_t)std::max(cooling_slots(), G + 1);
   const int flush = tuning().stream_flush >= 0 ? tuning().stream_flush : 0;
+  if (flush >= 3 && !d.tick_h) {
+    HIPCHK(c, hipHostMalloc((void**)&d.tick_h, 64, hipHostMallocDefault));
+    HIPCHK(c, hipMalloc((void**)&d.tick_d, 64));
+  }
   std::vector<SearchJob> jobs;
   jobs.reserve((size_t)G);
   int batch = 0;
@@ -250,6 +265,7 @@ me_status run_pairs(me_ctx* c, Dev& d, const Job& j, int p0, int p1) {
         }
         HIPCHK(c, hipEventRecord(d.slot_ready[si], d.copy));
         if (flush == 1) (void)hipStreamQuery(d.copy);
+        if (flush == 3) HIPCHK(c, hipMemcpyAsync(d.tick_d, d.tick_h, 64, hipMemcpyHostToDevice, d.copy));
         slot_of[f] = si;
       }
       const int sr = slot_of[j.pairs[2 * n]], sc = slot_of[j.pairs[2 * n + 1]];
@@ -262,6 +278,7 @@ me_status run_pairs(me_ctx* c, Dev& d, const Job& j, int p0, int p1) {
       jobs.push_back(SearchJob{d.slots[sr], 0, d.slots[sc], 0, 0, nby, out_mv + 2 * o, out_cost + o});
     }
     if (flush == 2) (void)hipStreamQuery(d.copy);
+    if (flush == 4) HIPCHK(c, hipMemcpyAsync(d.tick_d, d.tick_h, 64, hipMemcpyHostToDevice, d.copy));
     if ((s = me::attach_scratch(c, d, base, false, n1 - n0)) != ME_OK) return s;
     if ((s = me::launch_jobs_ordered(c, d, base, jobs.data(), n1 - n0, d.stream)) != ME_OK) return s;
     if (kAhead <= 8) HIPCHK(c, hipEventRecord(d.pair_ev[batch % kAhead], d.stream));

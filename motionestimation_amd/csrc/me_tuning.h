@@ -21,8 +21,11 @@ struct Tuning {
   int stream_cool = 0;    // ME_STREAM_COOL=1..64: cooling frame slots (0 = automatic)
   int stream_ahead = 0;   // ME_STREAM_AHEAD=1..9: host run-ahead (9: unbounded; 0 = automatic)
   int stream_batch = 0;   // ME_STREAM_BATCH=1..32: pairs per search launch (0 = automatic)
+  int stream_fence = -1;  // ME_STREAM_FENCE=0..2: pipeline events' release scope (0 system, 1 no
+                          // system fence, 2 device-scope release; -1 = automatic)
   int stream_flush = -1;  // ME_STREAM_FLUSH=0..3: how the copy stream's ready markers are pushed
-                          // (0 none, 1 hipStreamQuery after each upload, 2 once per batch; -1 = automatic)
+                          // (0 none, 1 hipStreamQuery after each upload, 2 once per batch, 3 a 64-byte
+                          // tick copy after each upload, 4 one after the batch's uploads; -1 = automatic)
   int flow = -1;          // ME_FLOW=0|1: SAD flow kernel off / allowed (-1 = automatic)
   int flow_slots = 0;     // ME_FLOW_SLOTS=2..16: flow kernel LDS ring slots (0 = automatic)
   int prio = -1;          // ME_PRIO=0|1: staging waves raise their issue priority (-1 = automatic: on)
@@ -30,6 +33,8 @@ struct Tuning {
                           // with refills (automatic), 2 on items whose slot gets a refill, 3 always
   int fair_lo = 8, fair_hi = 16;  // ME_FAIR_T=lo,hi: the lags (pulls) that raise a wave to priority 1 / 2
   int flow_one = -1;      // ME_FLOW_ONE=0|1: a batch's flow jobs in launches of one ring / in one launch (-1 = automatic: one)
+  int mfma_s2k = -1;      // ME_MFMA_S2K=0|1: 16x16 SSD, S <= 64: S2 from the prepass plane / formed in
+                          // the workgroup (-1 = automatic: in the workgroup)
   int mfma_batch = -1;    // ME_MFMA_BATCH=0|1: equal SSD jobs share matrix-core launches (-1 = automatic: on)
   int strip = -1;         // ME_STRIP=0..64: item-kernel tile strips (0 = row-major; -1 = automatic)
 };
