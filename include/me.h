@@ -94,10 +94,19 @@ const char* me_version(void);
  * everything else on the VALU kernels; ME_PATH_VALU: VALU kernels only;
  * ME_PATH_MFMA_TILES: as AUTO, but 16x16 SSD on the 4x4-block-tile MFMA kernel
  * (the fallback for rows that are not 16-byte aligned) instead of the
- * block-major one.  Results are identical on every path.  The environment
- * variable ME_PATH=auto|valu|tiles sets the initial value (anything else is
- * ignored with a message on stderr). */
-typedef enum { ME_PATH_AUTO = 0, ME_PATH_VALU = 1, ME_PATH_MFMA_TILES = 2 } me_path;
+ * block-major one; ME_PATH_MFMA_LEAN: as AUTO, but 16x16 SSD with S <= 64
+ * forms its S2 term inside the search kernel instead of reading the prepass
+ * planes: no context scratch (AUTO holds 5 bytes per reference pixel of it per
+ * frame of a batch) and ~1.2x the algorithmic HBM bytes instead of ~7.5x, at
+ * ~1.4x the kernel time.  Results are identical on every path.
+ * The environment variable ME_PATH=auto|valu|tiles|lean sets the initial value
+ * (anything else is ignored with a message on stderr). */
+typedef enum {
+  ME_PATH_AUTO = 0,
+  ME_PATH_VALU = 1,
+  ME_PATH_MFMA_TILES = 2,
+  ME_PATH_MFMA_LEAN = 3
+} me_path;
 void me_set_kernel_path(me_path path);
 
 /* Tiling helpers (src/common/prediction_frame.c:9-11). */

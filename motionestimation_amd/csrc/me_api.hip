@@ -63,8 +63,6 @@ static Tuning read_tuning() {
   env_int("ME_STREAM_COOL", 1, 64, &t.stream_cool);
   env_int("ME_STREAM_AHEAD", 1, 9, &t.stream_ahead);
   env_int("ME_STREAM_BATCH", 1, 32, &t.stream_batch);
-  env_int("ME_STREAM_FLUSH", 0, 4, &t.stream_flush);
-  env_int("ME_STREAM_FENCE", 0, 2, &t.stream_fence);
   env_int("ME_FLOW", 0, 1, &t.flow);
   env_int("ME_FLOW_SLOTS", 2, 16, &t.flow_slots);
   env_int("ME_PRIO", 0, 1, &t.prio);
@@ -101,7 +99,8 @@ static int initial_path() {
   if (!e || !*e || !strcmp(e, "auto")) return 0;
   if (!strcmp(e, "valu")) return 1;
   if (!strcmp(e, "tiles")) return 2;
-  fprintf(stderr, "me_hip: ignoring ME_PATH=%s (auto | valu | tiles)\n", e);
+  if (!strcmp(e, "lean")) return 3;
+  fprintf(stderr, "me_hip: ignoring ME_PATH=%s (auto | valu | tiles | lean)\n", e);
   return 0;
 }
 static std::atomic<int>& path_code() {
@@ -549,7 +548,8 @@ const char* me_last_error(const me_ctx* ctx) { return ctx ? ctx->err : "null con
 const char* me_version(void) { return "me_hip 1 gfx950"; }
 
 void me_set_kernel_path(me_path path) {
-  me::set_kernel_path_code(path == ME_PATH_VALU ? 1 : path == ME_PATH_MFMA_TILES ? 2 : 0);
+  me::set_kernel_path_code(path == ME_PATH_VALU ? 1 : path == ME_PATH_MFMA_TILES ? 2
+                           : path == ME_PATH_MFMA_LEAN ? 3 : 0);
 }
 
 me_status me_create(me_ctx** out, const int* device_ids, int n) {

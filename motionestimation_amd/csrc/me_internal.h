@@ -50,17 +50,17 @@ struct Dev {
   bool searched = false;
   // Frame-pair pipeline (me_stream.hip), kept across calls.
   std::vector<uint8_t*> slots;        // device frames, slot_bytes each
-  std::vector<hipEvent_t> slot_ready; // upload of the slot's frame done (copy stream)
-  std::vector<hipEvent_t> slot_free;  // last search reading the slot done (compute stream)
   size_t slot_bytes = 0;
   uint8_t* stage[2] = {nullptr, nullptr};  // pinned staging for pageable frames
   hipEvent_t stage_ev[2] = {nullptr, nullptr};
   size_t stage_bytes = 0;
-  hipEvent_t pair_ev[8] = {};  // search of pair n done: bounds how far the host runs ahead
+  // One event pair per batch of pairs (ring by batch index): the batch's uploads
+  // done (copy stream; the compute stream waits on it once) and its search done
+  // (compute stream; bounds the host's run-ahead and guards slot reuse).
+  hipEvent_t upl_ev[16] = {};
+  hipEvent_t batch_ev[16] = {};
   uint8_t* pair_out = nullptr;  // [pairs][nblocks] mv records, then [pairs][nblocks] costs
   size_t pair_out_cap = 0;
-  uint8_t* tick_h = nullptr;     // 64 pinned bytes: the copy stream's trailing tick copy
-  uint8_t* tick_d = nullptr;     //   (me_stream.hip) and its device target
   // An invariant report that a synchronous entry point read (and cleared on
   // the device) on behalf of earlier asynchronous searches: me_device_check
   // still reports it once (device_status sets it, me_device_check clears it).

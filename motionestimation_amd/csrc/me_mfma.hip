@@ -1741,9 +1741,10 @@ bool plan_mfma_ssd(const SearchArgs& p, MfmaGeom* g) {
   g->lds = 4 * (L + 15) * (64 * g->ngxw + 32) + 16 * 8 + 16 * 4 + L * 256 * g->ngxw;
   g->bm_wpr = (g->nbx + 7) / 8;
   if (g->bm) g->lds = BM_HDR + 2 * 31 * g->bm_lp;
-  // S <= 64 (window pitch 288): S2 formed in the workgroup, no prepass planes
-  // (ME_MFMA_S2K=0: the prepass kernel; tuning build)
-  g->bmv = g->bm && g->bm_lp == BMV_LP && tuning().mfma_s2k != 0;
+  // ME_PATH_MFMA_LEAN, S <= 64 (window pitch 288): S2 formed in the workgroup,
+  // no prepass planes (ME_MFMA_S2K=0|1 overrides; tuning build)
+  const int s2k = tuning().mfma_s2k >= 0 ? tuning().mfma_s2k : kernel_path() == 3;
+  g->bmv = g->bm && g->bm_lp == BMV_LP && s2k;
   if (g->bmv) g->lds = BMV_LDS;
   g->mkeys = p.mkeys;
   g->mcnt = p.mcnt;

@@ -15,6 +15,9 @@
 //     host-side staging and upload of pair n+1's new frame overlap the search
 //     of pair n (slots are reused oldest-freed first, so an upload never
 //     waits on the search it should overlap);
+//   - the streams are ordered by one event per batch each way (uploads done,
+//     search done), not per frame slot: event packets between two search
+//     launches delayed each launch by 58-74 us (profiles/r04e_*);
 //   - frames in me_host_alloc memory are DMAed directly, other frames are
 //     staged through two pinned buffers;
 //   - MV records stay in HBM until the run ends, then one copy per output.
@@ -43,14 +46,7 @@ std::map<uintptr_t, size_t> g_pinned;  // me_host_alloc ranges: base -> bytes
 static int cooling_slots() { return tuning().stream_cool > 0 ? tuning().stream_cool : 2; }
 // Pairs per search launch (ME_STREAM_BATCH overrides; tuning)
 constexpr int kPairBatch = 4;
-// Flags of the pipeline's ordering events (slot ready / slot free / pair done):
-// they order work of this device's own streams (and bound the host's run-ahead),
-// so a device-scope release is enough (ME_STREAM_FENCE overrides; tuning)
-unsigned pipe_event_flags() {
-  const int f = tuning().stream_fence >= 0 ? tuning().stream_fence : 0;
-  return hipEventDisableTiming |
-         (f == 1 ? hipEventDisableSystemFence : f == 2 ? hipEventReleaseToDevice : 0u);
-}
+constexpr int kEvRing = 16;  // batch events (Dev::upl_ev / batch_ev), ring by batch index
 }  // namespace
 
 bool host_range_pinned(const void* p, size_t bytes) {
@@ -64,18 +60,13 @@ bool host_range_pinned(const void* p, size_t bytes) {
 
 void release_pipeline(Dev& d) {
   if (d.copy) (void)hipStreamSynchronize(d.copy);
-  for (size_t i = 0; i < d.slots.size(); i++) {
-    (void)hipFree(d.slots[i]);
-    (void)hipEventDestroy(d.slot_ready[i]);
-    (void)hipEventDestroy(d.slot_free[i]);
-  }
-  for (auto& e : d.pair_ev) {
-    if (e) (void)hipEventDestroy(e);
-    e = nullptr;
+  for (size_t i = 0; i < d.slots.size(); i++) (void)hipFree(d.slots[i]);
+  for (int k = 0; k < kEvRing; k++) {
+    if (d.upl_ev[k]) (void)hipEventDestroy(d.upl_ev[k]);
+    if (d.batch_ev[k]) (void)hipEventDestroy(d.batch_ev[k]);
+    d.upl_ev[k] = d.batch_ev[k] = nullptr;
   }
   d.slots.clear();
-  d.slot_ready.clear();
-  d.slot_free.clear();
   d.slot_bytes = 0;
   for (int k = 0; k < 2; k++) {
     if (d.stage[k]) (void)hipHostFree(d.stage[k]);
@@ -87,9 +78,6 @@ void release_pipeline(Dev& d) {
   (void)hipFree(d.pair_out);
   d.pair_out = nullptr;
   d.pair_out_cap = 0;
-  if (d.tick_h) (void)hipHostFree(d.tick_h);
-  (void)hipFree(d.tick_d);
-  d.tick_h = d.tick_d = nullptr;
   if (d.copy) (void)hipStreamDestroy(d.copy);
   d.copy = nullptr;
 }
@@ -109,17 +97,15 @@ me_status prepare(me_ctx* c, Dev& d, size_t plane) {
   if (d.slot_bytes != plane) {  // frame size changed: drop the old slots
     HIPCHK(c, hipStreamSynchronize(d.stream));
     if (d.copy) HIPCHK(c, hipStreamSynchronize(d.copy));
-    for (size_t i = 0; i < d.slots.size(); i++) {
-      (void)hipFree(d.slots[i]);
-      (void)hipEventDestroy(d.slot_ready[i]);
-      (void)hipEventDestroy(d.slot_free[i]);
-    }
+    for (size_t i = 0; i < d.slots.size(); i++) (void)hipFree(d.slots[i]);
     d.slots.clear();
-    d.slot_ready.clear();
-    d.slot_free.clear();
     d.slot_bytes = plane;
   }
   if (!d.copy) HIPCHK(c, hipStreamCreateWithFlags(&d.copy, hipStreamNonBlocking));
+  for (int k = 0; k < kEvRing; k++) {
+    if (!d.upl_ev[k]) HIPCHK(c, hipEventCreateWithFlags(&d.upl_ev[k], hipEventDisableTiming));
+    if (!d.batch_ev[k]) HIPCHK(c, hipEventCreateWithFlags(&d.batch_ev[k], hipEventDisableTiming));
+  }
   return ME_OK;
 }
 
@@ -140,16 +126,7 @@ me_status new_slot(me_ctx* c, Dev& d, int* idx) {
   uint8_t* p = nullptr;
   if (hipMalloc((void**)&p, d.slot_bytes) != hipSuccess)
     return fail(c, ME_ENOMEM, "hipMalloc(%zu) for a frame slot failed", d.slot_bytes);
-  hipEvent_t r = nullptr, f = nullptr;
-  if (hipEventCreateWithFlags(&r, pipe_event_flags()) != hipSuccess ||
-      hipEventCreateWithFlags(&f, pipe_event_flags()) != hipSuccess) {
-    (void)hipFree(p);
-    if (r) (void)hipEventDestroy(r);
-    return fail(c, ME_EDEVICE, "hipEventCreate failed");
-  }
   d.slots.push_back(p);
-  d.slot_ready.push_back(r);
-  d.slot_free.push_back(f);
   *idx = (int)d.slots.size() - 1;
   return ME_OK;
 }
@@ -193,6 +170,9 @@ me_status run_pairs(me_ctx* c, Dev& d, const Job& j, int p0, int p1) {
   }
   std::deque<int> free_slots;  // oldest-freed first
   for (int i = 0; i < (int)d.slots.size(); i++) free_slots.push_back(i);
+  // per slot: the last batch of this call whose search read it (-1: none; the
+  // previous call ended with the device idle)
+  std::vector<int> last_batch(d.slots.size(), -1);
   int stage_k = 0;
   const size_t span = (size_t)(H - 1) * j.stride + W;
 
@@ -210,8 +190,6 @@ me_status run_pairs(me_ctx* c, Dev& d, const Job& j, int p0, int p1) {
                    host_range_pinned(j.frames[j.pairs[2 * n + side]], (size_t)(H - 1) * j.stride + W);
   const int env_ahead = tuning().stream_ahead;  // tuning build: 1..8, 9 unbounded (diagnostic)
   const int kAhead = env_ahead > 8 ? 1 << 30 : env_ahead >= 1 ? env_ahead : (all_pinned ? 2 : 3);
-  for (auto& e : d.pair_ev)
-    if (!e) HIPCHK(c, hipEventCreateWithFlags(&e, pipe_event_flags()));
   // Pairs are searched G at a time in one job-table launch (launch_jobs: the
   // flow / item kernels' job tables, SSD pairs sharing the matrix cores'
   // launches), so a launch's fill and drain are paid once per G pairs.  The
@@ -219,19 +197,26 @@ me_status run_pairs(me_ctx* c, Dev& d, const Job& j, int p0, int p1) {
   // ones: at least G + 1 of them.
   const int G = tuning().stream_batch > 0 ? tuning().stream_batch : kPairBatch;
   const size_t cool = (size_t)std::max(cooling_slots(), G + 1);
-  const int flush = tuning().stream_flush >= 0 ? tuning().stream_flush : 0;
-  if (flush >= 3 && !d.tick_h) {
-    HIPCHK(c, hipHostMalloc((void**)&d.tick_h, 64, hipHostMallocDefault));
-    HIPCHK(c, hipMalloc((void**)&d.tick_d, 64));
-  }
+  // Ordering events: one per batch on each stream, not one per frame slot.
+  // The round-3 scheme (a ready event per upload, a free event per released
+  // slot, one wait per frame of every pair) put ~13 event packets between two
+  // search launches on the compute stream and a wait + record around every
+  // upload on the copy stream; the trace showed each search starting 58-74 us
+  // after the previous one ended although its uploads had landed 150 us
+  // earlier, and ~17 us between consecutive uploads (profiles/r04e_*).
+  int synced = -1;  // newest batch the host has waited for
   std::vector<SearchJob> jobs;
   jobs.reserve((size_t)G);
   int batch = 0;
   for (int n0 = p0; n0 < p1; n0 += G, batch++) {
     const int n1 = std::min(p1, n0 + G);
-    if (kAhead <= 8 && batch >= kAhead) HIPCHK(c, hipEventSynchronize(d.pair_ev[batch % kAhead]));
+    if (kAhead <= 8 && batch >= kAhead) {
+      HIPCHK(c, hipEventSynchronize(d.batch_ev[(batch - kAhead) % kEvRing]));
+      synced = batch - kAhead;
+    }
     jobs.clear();
     me::SearchArgs base{};
+    int uploads = 0;
     for (int n = n0; n < n1; n++) {
       for (int side = 0; side < 2; side++) {
         const int f = j.pairs[2 * n + side];
@@ -241,10 +226,14 @@ me_status run_pairs(me_ctx* c, Dev& d, const Job& j, int p0, int p1) {
         int si;
         if (free_slots.size() < cool) {
           if ((s = new_slot(c, d, &si)) != ME_OK) return s;
+          last_batch.push_back(-1);
         } else {
           si = free_slots.front();
           free_slots.pop_front();
-          HIPCHK(c, hipStreamWaitEvent(d.copy, d.slot_free[si], 0));
+          // its last reader may still run only if the host has not waited for
+          // it yet (a later batch's event in the ring covers it too: in order)
+          const int lb = last_batch[si];
+          if (lb > synced) HIPCHK(c, hipStreamWaitEvent(d.copy, d.batch_ev[lb % kEvRing], 0));
         }
         const uint8_t* src = j.frames[f];
         if (host_range_pinned(src, span)) {
@@ -263,31 +252,31 @@ me_status run_pairs(me_ctx* c, Dev& d, const Job& j, int p0, int p1) {
           HIPCHK(c, hipEventRecord(d.stage_ev[stage_k], d.copy));
           stage_k ^= 1;
         }
-        HIPCHK(c, hipEventRecord(d.slot_ready[si], d.copy));
-        if (flush == 1) (void)hipStreamQuery(d.copy);
-        if (flush == 3) HIPCHK(c, hipMemcpyAsync(d.tick_d, d.tick_h, 64, hipMemcpyHostToDevice, d.copy));
+        uploads++;
         slot_of[f] = si;
       }
       const int sr = slot_of[j.pairs[2 * n]], sc = slot_of[j.pairs[2 * n + 1]];
-      HIPCHK(c, hipStreamWaitEvent(d.stream, d.slot_ready[sr], 0));
-      if (sc != sr) HIPCHK(c, hipStreamWaitEvent(d.stream, d.slot_ready[sc], 0));
       const size_t o = (size_t)(n - p0) * nb;
       if (n == n0)
         base = make_args(d.slots[sr], 0, d.slots[sc], 0, W, H, W, B, j.range, j.cost, 0, nby,
                          out_mv + 2 * o, out_cost + o);
       jobs.push_back(SearchJob{d.slots[sr], 0, d.slots[sc], 0, 0, nby, out_mv + 2 * o, out_cost + o});
     }
-    if (flush == 2) (void)hipStreamQuery(d.copy);
-    if (flush == 4) HIPCHK(c, hipMemcpyAsync(d.tick_d, d.tick_h, 64, hipMemcpyHostToDevice, d.copy));
+    // one wait for this batch's uploads (the copy stream is in order: frames
+    // uploaded by earlier batches were covered by their batches' waits)
+    if (uploads) {
+      HIPCHK(c, hipEventRecord(d.upl_ev[batch % kEvRing], d.copy));
+      HIPCHK(c, hipStreamWaitEvent(d.stream, d.upl_ev[batch % kEvRing], 0));
+    }
     if ((s = me::attach_scratch(c, d, base, false, n1 - n0)) != ME_OK) return s;
     if ((s = me::launch_jobs_ordered(c, d, base, jobs.data(), n1 - n0, d.stream)) != ME_OK) return s;
-    if (kAhead <= 8) HIPCHK(c, hipEventRecord(d.pair_ev[batch % kAhead], d.stream));
+    HIPCHK(c, hipEventRecord(d.batch_ev[batch % kEvRing], d.stream));
     for (int n = n0; n < n1; n++)
       for (int side = 0; side < 2; side++) {
         const int f = j.pairs[2 * n + side];
         if (last_use[f] < n1 && slot_of[f] >= 0) {
           const int si = slot_of[f];
-          HIPCHK(c, hipEventRecord(d.slot_free[si], d.stream));
+          last_batch[si] = batch;
           free_slots.push_back(si);
           slot_of[f] = -1;
         }

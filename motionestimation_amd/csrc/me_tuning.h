@@ -21,11 +21,6 @@ struct Tuning {
   int stream_cool = 0;    // ME_STREAM_COOL=1..64: cooling frame slots (0 = automatic)
   int stream_ahead = 0;   // ME_STREAM_AHEAD=1..9: host run-ahead (9: unbounded; 0 = automatic)
   int stream_batch = 0;   // ME_STREAM_BATCH=1..32: pairs per search launch (0 = automatic)
-  int stream_fence = -1;  // ME_STREAM_FENCE=0..2: pipeline events' release scope (0 system, 1 no
-                          // system fence, 2 device-scope release; -1 = automatic)
-  int stream_flush = -1;  // ME_STREAM_FLUSH=0..3: how the copy stream's ready markers are pushed
-                          // (0 none, 1 hipStreamQuery after each upload, 2 once per batch, 3 a 64-byte
-                          // tick copy after each upload, 4 one after the batch's uploads; -1 = automatic)
   int flow = -1;          // ME_FLOW=0|1: SAD flow kernel off / allowed (-1 = automatic)
   int flow_slots = 0;     // ME_FLOW_SLOTS=2..16: flow kernel LDS ring slots (0 = automatic)
   int prio = -1;          // ME_PRIO=0|1: staging waves raise their issue priority (-1 = automatic: on)
@@ -34,7 +29,7 @@ struct Tuning {
   int fair_lo = 8, fair_hi = 16;  // ME_FAIR_T=lo,hi: the lags (pulls) that raise a wave to priority 1 / 2
   int flow_one = -1;      // ME_FLOW_ONE=0|1: a batch's flow jobs in launches of one ring / in one launch (-1 = automatic: one)
   int mfma_s2k = -1;      // ME_MFMA_S2K=0|1: 16x16 SSD, S <= 64: S2 from the prepass plane / formed in
-                          // the workgroup (-1 = automatic: in the workgroup)
+                          // the workgroup (-1 = automatic: the kernel path, ME_PATH_MFMA_LEAN)
   int mfma_batch = -1;    // ME_MFMA_BATCH=0|1: equal SSD jobs share matrix-core launches (-1 = automatic: on)
   int strip = -1;         // ME_STRIP=0..64: item-kernel tile strips (0 = row-major; -1 = automatic)
 };
@@ -42,7 +37,8 @@ struct Tuning {
 const Tuning& tuning();
 
 // Kernel path (me_set_kernel_path / ME_PATH): 0 automatic, 1 VALU kernels only,
-// 2 no block-major MFMA kernel.  Atomic: read by planner threads.
+// 2 no block-major MFMA kernel, 3 block-major with S2 in the workgroup (lean).
+// Atomic: read by planner threads.
 int kernel_path();
 void set_kernel_path_code(int v);
 

@@ -47,8 +47,11 @@ def plan_stripes(width: int, height: int, blk: int, span: int, shards: int) -> l
 def set_kernel_path(path: str) -> None:
     """'auto': 16x16 and 8x8 SSD on the matrix cores (i8 MFMA), the rest on
     the VALU kernels; 'valu': VALU kernels only; 'tiles': as 'auto' with 16x16
-    SSD on the 4x4-block-tile MFMA kernel.  Process-wide; results are identical."""
-    codes = {"auto": _lib.ME_PATH_AUTO, "valu": _lib.ME_PATH_VALU, "tiles": _lib.ME_PATH_MFMA_TILES}
+    SSD on the 4x4-block-tile MFMA kernel; 'lean': as 'auto' with 16x16 SSD
+    (S <= 64) forming S2 in the search kernel (no prepass planes, no scratch).
+    Process-wide; results are identical."""
+    codes = {"auto": _lib.ME_PATH_AUTO, "valu": _lib.ME_PATH_VALU, "tiles": _lib.ME_PATH_MFMA_TILES,
+             "lean": _lib.ME_PATH_MFMA_LEAN}
     if path not in codes:
         raise MEError(_lib.ME_EINVAL, f"unknown kernel path {path!r}")
     _lib.lib().me_set_kernel_path(codes[path])

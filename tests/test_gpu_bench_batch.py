@@ -62,8 +62,14 @@ def test_headline_batch_1080p_sad_equals_oracle_every_frame(engine):
         assert _hash(mv, co, 1920, 1080, 16, "sad") == pins[f], f"frame {f} pin"
 
 
-def test_ssd_leg_batch_1080p_equals_reference_every_frame(engine):
-    fields = _search(engine, _batch("1080p"), 16, 32, "ssd")
+@pytest.mark.parametrize("path", ["auto", "lean"])
+def test_ssd_leg_batch_1080p_equals_reference_every_frame(engine, path):
+    import motionestimation_amd as me
+    me.set_kernel_path(path)
+    try:
+        fields = _search(engine, _batch("1080p"), 16, 32, "ssd")
+    finally:
+        me.set_kernel_path("auto")
     pins = bench.load_pins("1080p", 16, 32, "ssd")
     assert len(pins) == F
     bad = [f for f, (mv, co) in enumerate(fields) if _hash(mv, co, 1920, 1080, 16, "ssd") != pins[f]]
@@ -71,12 +77,17 @@ def test_ssd_leg_batch_1080p_equals_reference_every_frame(engine):
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("cost", ["sad", "ssd"])
-def test_stripe_4k_batch_equals_pins(engine, cost):
+@pytest.mark.parametrize("cost,path", [("sad", "auto"), ("ssd", "auto"), ("ssd", "lean")])
+def test_stripe_4k_batch_equals_pins(engine, cost, path):
+    import motionestimation_amd as me
     pins = bench.load_pins("4k", 16, 64, cost)
     if not pins:
         pytest.skip("no 4K pins committed")
-    fields = _search(engine, _batch("4k"), 16, 64, cost)
+    me.set_kernel_path(path)
+    try:
+        fields = _search(engine, _batch("4k"), 16, 64, cost)
+    finally:
+        me.set_kernel_path("auto")
     bad = [f for f, (mv, co) in enumerate(fields[:len(pins)])
            if _hash(mv, co, 3840, 2160, 16, cost) != pins[f]]
     assert not bad, f"4K {cost} frames {bad} differ from their pins"

@@ -1,5 +1,6 @@
-"""Matrix-core SSD path (me_mfma.hip: i8 MFMA cross term + S2 prepass) against
-the oracle and against the VALU kernels, bit-exact (MVs and integer SSDs).
+"""Matrix-core SSD path (me_mfma.hip: i8 MFMA cross term + S2 prepass, or S2
+formed in the search kernel on the lean path) against the oracle and against
+the VALU kernels, bit-exact (MVs and integer SSDs).
 
 The MFMA path serves B = 16 SSD on full blocks; tiles of 4x4 blocks, chunks of
 L = 45/61 candidate rows, 1-4 groups of 64 candidate columns (S up to 103).
@@ -19,6 +20,16 @@ from motionestimation_amd import synth
 
 pytestmark = pytest.mark.gpu
 NT = min(16, os.cpu_count() or 1)
+
+
+@pytest.fixture(params=["auto", "lean"], autouse=True)
+def ssd_path(request):
+    """Every case on the default matrix-core path (prepass planes) and on the
+    lean one (ME_PATH_MFMA_LEAN: 16x16, S <= 64 forms S2 in the search kernel;
+    other shapes plan as auto).  Cases that switch paths themselves end on auto."""
+    me.set_kernel_path(request.param)
+    yield request.param
+    me.set_kernel_path("auto")
 
 
 def _pair(rng, h, w, dx=2, dy=-1, noise=3):

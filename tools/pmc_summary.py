@@ -90,6 +90,8 @@ blk, span = {"1080p": (16, 32), "4k": (16, 64), "8k": (8, 128)}[cfg]
 # keyed like bench.py's lookup: the workload and its frames per step (a SAD
 # launch holds every frame of the step, an SSD launch one frame)
 bench_tag = f"{cfg}_b{blk}_s{span}_{cost}_f{frames}"
+if os.environ.get("ME_PATH") == "lean":  # the lean matrix-core SSD path (S2 in the search kernel)
+    bench_tag += "_lean"
 path = os.path.join(PROF, "pmc_summary.json")
 try:
     allsum = json.load(open(path))
