@@ -1258,12 +1258,12 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_bm16_kernel(SearchArgs p, M
 // bytes of a 1080p search, DESIGN.md "SSD-path HBM traffic").  The band window
 // is DMA'd from the reference plane itself, and every band's S2 is formed in
 // LDS from the window the band already holds:
-//   phase A  lane = position p: H(row, p) = sum_{4 bytes} (r^2 - 254 r), two
-//            v_dot4 per row; V(k, p) = sum_{i < hb} H(k + i, p) by a sliding
-//            sum down the 15 + hb window rows (raw bytes: it runs before the
-//            window is XOR-ed)
-//   phase B  S2(k, x) = V(k, x) + V(k, x + 4) + V(k, x + 8) + V(k, x + 12)
-//            (+ 256 * 127^2, folded into the key constant), in place
+//   phase A  lane = position p: with u = r ^ 0x7F = 127 - r (an exact i8),
+//            (r - 127)^2 = u^2, so H(row, p) = sum_{4 bytes} u^2 is ONE v_dot4
+//            (plus the XOR and the v_alignbyte of the position's 4 bytes);
+//            V(k, p) = sum_{i < hb} H(k + i, p) by a sliding sum down the
+//            15 + hb window rows (raw bytes: it runs before the window is XOR-ed)
+//   phase B  S2(k, x) = V(k, x) + V(k, x + 4) + V(k, x + 8) + V(k, x + 12), in place
 //   the window's bytes are XOR-ed with 0x80 (r' = r - 128, the B operand)
 // The tiles then read S2 from LDS instead of the plane.  crec (the cur row
 // records) aliases the S2 plane: the A fragments are built before band 0.
@@ -1274,12 +1274,11 @@ constexpr int BMV_KEYS = 8 * 8 + 8 * 4;    // keys, cc
 constexpr int BMV_LP = 288;
 constexpr int BMV_LDS = BMV_KEYS + BMV_PLANE + 2 * 31 * BMV_LP;
 static_assert(8 * 16 * BM_CREC <= BMV_PLANE, "crec aliases the S2 plane");
-constexpr int BMV_S2C = 256 * 127 * 127;   // the constant part of S2 = sum (r - 127)^2
-
-// r^2 - 254 r summed over the 4 bytes of v (S2 = sum of these + 256 * 127^2)
-__device__ __forceinline__ int h4(uint32_t v) {
-  return (int)__builtin_amdgcn_udot4(v, v, 0u, false) -
-         (int)__builtin_amdgcn_udot4(v, 0xFEFEFEFEu, 0u, false);
+// acc + sum over the 4 bytes r of v of (r - 127)^2: u = r ^ 0x7F is 127 - r as
+// an i8 (r in [0, 255] -> u in [-128, 127]), and u^2 = (r - 127)^2
+__device__ __forceinline__ int h4acc(uint32_t v, int acc) {
+  const int u = (int)(v ^ 0x7F7F7F7Fu);
+  return __builtin_amdgcn_sdot4(u, u, acc, false);
 }
 
 // Phase A, 16-row blocks: V(k, p) for the 16 band rows k, position p (window
@@ -1300,22 +1299,20 @@ __device__ __forceinline__ void bmv_vsum16(const uint8_t* win, int p, int* vcol)
   int v = 0;
 #pragma unroll
   for (int k = 0; k < 16; k++) {
-    const int hk = h4(row(k));
-    vcol[k * BMV_NP] = hk;
-    v += hk;
+    const int nv = h4acc(row(k), v);
+    if (k < 15) vcol[k * BMV_NP] = nv - v;  // H(k)
+    v = nv;
   }
 #pragma unroll
   for (int k = 1; k < 16; k++) {
     const int old = vcol[(k - 1) * BMV_NP];
     vcol[(k - 1) * BMV_NP] = v;
-    v += h4(row(k + 15)) - old;
+    v = h4acc(row(k + 15), v) - old;
   }
   vcol[15 * BMV_NP] = v;
 }
 
 // Phase A for a partial bottom block row (block height hb < 16): direct sums.
-// S2 there has hb * 16 * 127^2 as its constant, not the 256 * 127^2 the key
-// constant holds: each of the four V terms of an S2 carries a quarter of the difference.
 template <int LP>
 __device__ __forceinline__ void bmv_vsum_hb(const uint8_t* win, int p, int hb, int* vcol) {
   typedef __attribute__((address_space(3))) const uint32_t lds_c32;
@@ -1323,11 +1320,11 @@ __device__ __forceinline__ void bmv_vsum_hb(const uint8_t* win, int p, int hb, i
                      (uint32_t)(p & ~3);
   const uint32_t sh = (uint32_t)(p & 3);
   for (int k = 0; k < 16; k++) {
-    int v = -(16 - hb) * 4 * 127 * 127;
+    int v = 0;
     for (int i = 0; i < hb; i++) {
       const uint32_t o = a + (uint32_t)((k + i) * LP);
-      v += h4(__builtin_amdgcn_alignbyte(*reinterpret_cast<lds_c32*>((uintptr_t)(o + 4u)),
-                                         *reinterpret_cast<lds_c32*>((uintptr_t)o), sh));
+      v = h4acc(__builtin_amdgcn_alignbyte(*reinterpret_cast<lds_c32*>((uintptr_t)(o + 4u)),
+                                           *reinterpret_cast<lds_c32*>((uintptr_t)o), sh), v);
     }
     vcol[k * BMV_NP] = v;
   }
@@ -1562,10 +1559,9 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_bmv_kernel(SearchArgs p, Mf
           f0 = n0;
           f1 = n1;
         }
-        // key = ((2 acc + S2 + 1 + 2^23) << 6) + 4 ((i - iu0) & 15) + r with
-        // S2 = s2c + 256 * 127^2 (the constant in kb)
+        // key = ((2 acc + S2 + 1 + 2^23) << 6) + 4 ((i - iu0) & 15) + r
         const int rel = i - iu0;
-        const uint32_t kb = (1u << 29) + 64u + ((uint32_t)BMV_S2C << 6) + 4u * (uint32_t)(rel & 15);
+        const uint32_t kb = (1u << 29) + 64u + 4u * (uint32_t)(rel & 15);
         uint32_t P[4];
 #pragma unroll
         for (int r = 0; r < 4; r++) P[r] = lshl6_add((uint32_t)s2c[r], kb + (uint32_t)r);

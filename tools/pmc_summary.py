@@ -92,6 +92,7 @@ blk, span = {"1080p": (16, 32), "4k": (16, 64), "8k": (8, 128)}[cfg]
 bench_tag = f"{cfg}_b{blk}_s{span}_{cost}_f{frames}"
 if os.environ.get("ME_PATH") == "lean":  # the lean matrix-core SSD path (S2 in the search kernel)
     bench_tag += "_lean"
+bench_tag += os.environ.get("PMC_KEY_SUFFIX", "")  # A/B variants (tuning-build settings)
 path = os.path.join(PROF, "pmc_summary.json")
 try:
     allsum = json.load(open(path))
