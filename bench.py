@@ -270,7 +270,19 @@ def host_stream(eng, w, h, blk, span, cost, seed, sx, sy, frame_ms, batch_frame_
     return out
 
 
-def single_frame(eng, ref_t, cur_t, blk, span, cost, nb, cands_frame, dev, steps, pins):
+def warm(fn, ms):
+    """Untimed calls of fn for `ms` of wall time (synchronising every 4): the
+    GPU clock drops during host-side gaps (the parity checks between legs) and
+    takes ~25 ms of load to come back (profiles/r03m_clock_ramp.json)."""
+    import torch
+    t0 = time.perf_counter()
+    while (time.perf_counter() - t0) * 1e3 < ms:
+        for _ in range(4):
+            fn()
+        torch.cuda.synchronize()
+
+
+def single_frame(eng, ref_t, cur_t, blk, span, cost, nb, cands_frame, dev, steps, pins, ramp_ms):
     """One frame per launch on the same resident pair (HIP events on the
     launch stream): what batching saves is launch gaps and per-launch tails.
     The last timed search's field is checked against pins[0] (ref_t is frame 0)."""
@@ -278,8 +290,7 @@ def single_frame(eng, ref_t, cur_t, blk, span, cost, nb, cands_frame, dev, steps
     h, w = ref_t.shape
     mv = torch.empty((nb, 2), dtype=torch.int16, device=dev)
     co = torch.empty(nb, dtype=torch.int32, device=dev)
-    for _ in range(3):
-        eng.full_search_device(ref_t, cur_t, blk, span, cost, mv, co)
+    warm(lambda: eng.full_search_device(ref_t, cur_t, blk, span, cost, mv, co), ramp_ms)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     e0.record()
@@ -295,7 +306,7 @@ def single_frame(eng, ref_t, cur_t, blk, span, cost, nb, cands_frame, dev, steps
             "parity": par}
 
 
-def ssd_beside(eng, ref_t, cur_t, blk, span, nb, cands_frame, dev, steps, pins):
+def ssd_beside(eng, ref_t, cur_t, blk, span, nb, cands_frame, dev, steps, pins, ramp_ms):
     """The reference's own cost (MSE = SSD / 256) on the step's resident frame
     pairs ([F, H, W] stacks): B = 16 SSD runs on the matrix cores (i8 MFMA), the
     F frames in one batched call (one prepass and one block-major launch).
@@ -307,8 +318,7 @@ def ssd_beside(eng, ref_t, cur_t, blk, span, nb, cands_frame, dev, steps, pins):
     mv = torch.empty((F * nb, 2), dtype=torch.int16, device=dev)
     co = torch.empty(F * nb, dtype=torch.int32, device=dev)
     run = eng.prepared_batch_search(ref_t, 0, cur_t, 0, w, h, blk, span, "ssd", 0, nby, mv, co)
-    for _ in range(3):
-        run()
+    warm(run, ramp_ms)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     e0.record()
@@ -994,12 +1004,14 @@ def main():
         # the same search one frame per launch (me_full_search_device), for
         # comparison: the batch's only difference is launches per frame
         line["single_frame"] = single_frame(eng, ref_t[0], cur_t[0], blk, span, args.cost, nb,
-                                            cands_frame, dev, min(args.steps * F, 100), pins)
+                                            cands_frame, dev, min(args.steps * F, 100), pins,
+                                            args.ramp_ms)
         legs["single_frame"] = line["single_frame"]["parity"]
     if (rank == 0 and world == 1 and mode == "frames" and args.cost == "sad"
             and blk == 16 and not args.no_ssd):
         line["ssd_mfma"] = ssd_beside(eng, ref_t, cur_t, blk, span, nb, cands_frame, dev,
-                                      min(args.steps, 20), load_pins(args.config, blk, span, "ssd"))
+                                      min(args.steps, 20), load_pins(args.config, blk, span, "ssd"),
+                                      args.ramp_ms)
         legs["ssd_mfma"] = line["ssd_mfma"]["parity"]
     if rank == 0 and world == 1 and not args.no_cpu:
         line["cpu_baseline"], field = cpu_baselines(ref, cur, blk, span, args.cost,
