@@ -71,6 +71,7 @@ static Tuning read_tuning() {
   env_int("ME_FLOW_ONE", 0, 1, &t.flow_one);
   env_int("ME_MFMA_BATCH", 0, 1, &t.mfma_batch);
   env_int("ME_MFMA_S2K", 0, 1, &t.mfma_s2k);
+  env_int("ME_MFMA_S2R", 1, 2, &t.mfma_s2r);
   if (const char* e = getenv("ME_FAIR_T")) {
     int lo = 0, hi = 0;
     if (sscanf(e, "%d,%d", &lo, &hi) == 2 && lo >= 1 && lo <= hi && hi <= 255) {

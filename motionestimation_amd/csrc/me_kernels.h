@@ -132,6 +132,7 @@ struct MfmaGeom {
   int km;                // candidate rows per chunk L = 13 + 16 km
   int bm, bm_wpr, bm_lp; // block-major kernel (16x16, S <= 192); workgroups per block row; window pitch
   int bmv;               // block-major kernel forming S2 itself (S <= 64): no prepass, no scratch
+  int bmv_r;             // ... its block rows per workgroup (1 or 2)
   int lds;               // dynamic LDS bytes
   int hb, hb_row;        // partial bottom block row: height hb, block row index (-1: none)
   int ya0, rp_rows;      // frame rows [ya0, ya0 + rp_rows) of the prepass planes

@@ -1270,10 +1270,7 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_bm16_kernel(SearchArgs p, M
 // S <= 64 (window pitch 288): LDS 35 KB, four workgroups per CU as before.
 constexpr int BMV_NP = 268;                // S2 / V plane row pitch (ints): 256 positions + 12 V; 67 * 4
 constexpr int BMV_PLANE = 16 * BMV_NP * 4; // 17,152 bytes (>= the 6,144 of crec)
-constexpr int BMV_KEYS = 8 * 8 + 8 * 4;    // keys, cc
 constexpr int BMV_LP = 288;
-constexpr int BMV_LDS = BMV_KEYS + BMV_PLANE + 2 * 31 * BMV_LP;
-static_assert(8 * 16 * BM_CREC <= BMV_PLANE, "crec aliases the S2 plane");
 // acc + sum over the 4 bytes r of v of (r - 127)^2: u = r ^ 0x7F is 127 - r as
 // an i8 (r in [0, 255] -> u in [-128, 127]), and u^2 = (r - 127)^2
 __device__ __forceinline__ int h4acc(uint32_t v, int acc) {
@@ -1286,8 +1283,11 @@ __device__ __forceinline__ int h4acc(uint32_t v, int acc) {
 template <int LP>
 __device__ __forceinline__ void bmv_vsum16(const uint8_t* win, int p, int* vcol) {
   typedef __attribute__((address_space(3))) const uint32_t lds_c32;
-  const uint32_t a = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) const uint8_t*)win) +
-                     (uint32_t)(p & ~3);
+  // opaque: one base per call, the rows at immediate offsets (hoisted, the 31
+  // row addresses were kept live across the band loop and spilled)
+  const uint32_t a = (uint32_t)opaque(
+      (int)((uint32_t)(uintptr_t)((__attribute__((address_space(3))) const uint8_t*)win) +
+            (uint32_t)(p & ~3)));
   const uint32_t sh = (uint32_t)(p & 3);
   auto row = [&](int k) {
     const uint32_t d0 = *reinterpret_cast<lds_c32*>((uintptr_t)(a + (uint32_t)(k * LP)));
@@ -1330,19 +1330,37 @@ __device__ __forceinline__ void bmv_vsum_hb(const uint8_t* win, int p, int hb, i
   }
 }
 
-__global__ __launch_bounds__(256)
+// Workgroup = R block rows (R = 1 or 2) x 8 blocks, 4 waves per row.  The y
+// bands are the workgroup's: Y_s = ylo (of its first row) + 16 s, so a band's
+// S2 is formed once for every row whose range it meets (R = 2: 6 bands for two
+// rows at S = 32 instead of 5 + 5).  A row skips the bands outside its range
+// and masks the rows of a band that leave it (bit 31 of the key).  A partial
+// bottom block row (height hb) reads a second S2 plane of hb-row sums when it
+// shares the workgroup with a full row.
+template <int R>
+constexpr int bmv_lds() {
+  return R * (8 * 8 + 8 * 4) + (R == 2 ? 2 : 1) * BMV_PLANE + 2 * 31 * BMV_LP;
+}
+
+template <int R>
+__global__ __launch_bounds__(256 * R)
 __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_bmv_kernel(SearchArgs p, MfmaGeom g, MfmaJobs jb) {
   constexpr int LP = BMV_LP;
   constexpr int WINB = 31 * LP;  // one band's window rows
+  constexpr int NT = 256 * R;    // threads
+  constexpr int KEYS = R * (8 * 8 + 8 * 4);
+  static_assert(R * 8 * 16 * BM_CREC <= BMV_PLANE, "crec aliases the S2 plane");
   extern __shared__ __align__(16) uint8_t smem[];
-  unsigned long long* keys = reinterpret_cast<unsigned long long*>(smem);
-  int* cc = reinterpret_cast<int*>(smem + 64);
-  int* plane = reinterpret_cast<int*>(smem + BMV_KEYS);  // S2 (phase B) / V (phase A), [16][BMV_NP]
-  uint8_t* crec = smem + BMV_KEYS;                       // until the A fragments are built
-  uint8_t* win = smem + BMV_KEYS + BMV_PLANE;
+  unsigned long long* keys = reinterpret_cast<unsigned long long*>(smem);  // [R * 8]
+  int* cc = reinterpret_cast<int*>(smem + R * 64);                          // [R * 8]
+  int* plane = reinterpret_cast<int*>(smem + KEYS);  // S2 (phase B) / V (phase A), [16][BMV_NP]
+  int* plane2 = reinterpret_cast<int*>(smem + KEYS + BMV_PLANE);  // R = 2: hb-row sums
+  uint8_t* crec = smem + KEYS;                                    // until the A fragments are built
+  uint8_t* win = smem + KEYS + (R == 2 ? 2 : 1) * BMV_PLANE;
 
   const int tid = (int)threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int rw = wave >> 2, wl = wave & 3;  // the wave's row in the workgroup, its place in the row
   const int n = lane & 15, h = lane >> 4;
   const int S = p.range, W = p.width, H = p.height;
   int lin;
@@ -1356,87 +1374,103 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_bmv_kernel(SearchArgs p, Mf
     lin -= j * jb.wgs;
     mfma_job(jb, j, p, g);
   }
-  const int brl = lin / g.bm_wpr, sx = lin - brl * g.bm_wpr;
-  const int br = g.row0 + brl;
+  const int grp = lin / g.bm_wpr, sx = lin - grp * g.bm_wpr;
+  const int br0 = g.row0 + R * grp;
+  const int nrw = min(R, g.row0 + g.nrows - br0);  // rows present (1 or R)
   const int bc0 = 8 * sx, nb = min(8, g.nbx - bc0);
-  const int by = 16 * br, bh = br == g.hb_row ? g.hb : 16;
-  const int ylo = max(by - S, 0), yhi = min(by + S, H - bh);
-  const int Ty = (yhi - ylo + 16) >> 4;
+  auto row_bh = [&](int r) { return br0 + r == g.hb_row ? g.hb : 16; };
+  auto row_ylo = [&](int r) { return max(16 * (br0 + r) - S, 0); };
+  auto row_yhi = [&](int r) { return min(16 * (br0 + r) + S, H - row_bh(r)); };
+  const int ylo = row_ylo(0);
+  const int yhi_w = row_yhi(nrw - 1) > row_yhi(0) ? row_yhi(nrw - 1) : row_yhi(0);
+  const int T = (yhi_w - ylo + 16) >> 4;  // workgroup bands
+  // S2 planes: plane for row 0's block height, plane2 for row 1's when it differs
+  const int bh0 = row_bh(0);
+  const bool two = R == 2 && nrw == 2 && row_bh(1) != bh0;
   const int tc0 = max(16 * bc0 - S, 0) >> 4;
-  // positions the workgroup's tiles read: 16 (tile of the last block's x range
-  // end - tc0 + 1); V is needed 12 positions further
   const int npos = 16 * ((min(16 * (bc0 + nb - 1) + S, W - 16) >> 4) - tc0 + 1);
   const int npv = npos + 12;
-  const bool yover = yhi - ylo >= 15;
-  auto band_y = [&](int s) { return yover ? min(ylo + 16 * s, yhi - 15) : ylo + 16 * s; };
-  // band window: frame rows [Ys, Ys + 31) x columns [16 tc0, 16 tc0 + LP) of the
-  // reference plane (rows past the resident ones read as zeros: masked), double-buffered
+  auto band_y = [&](int s) { return ylo + 16 * s; };
   const __amdgpu_buffer_rsrc_t rref =
       __builtin_amdgcn_make_buffer_rsrc((void*)p.ref, (short)0, p.ref_bytes, 0x00020000);
   auto stage_band = [&](int s) {
     const int gbase = (band_y(s) - p.ref_row0) * p.stride + 16 * tc0;
-    dma16(rref, win + (s & 1) * WINB, WINB, [&](int d) {
-      const int rho = d / LP, k = d - rho * LP;
-      return (uint32_t)(gbase + rho * p.stride + k);
-    });
+    const int lane16 = opaque(tid);
+    for (int s0 = (lane16 >> 6) * 1024; s0 < WINB; s0 += NT * 16) {
+      const int d = s0 + 16 * (lane16 & 63);
+      if (d < WINB) {
+        const int rho = d / LP, k = d - rho * LP;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rref, (__attribute__((address_space(3))) void*)(win + (s & 1) * WINB + s0), 16,
+            (uint32_t)(gbase + rho * p.stride + k), 0, 0, 0);
+      }
+    }
   };
   // S2 of band s (its window has landed in buffer s & 1; everyone is past the
   // previous band's tiles): V, then S2 in place, and the window XOR-ed for the MFMAs.
   auto band_s2 = [&](int s) {
     uint8_t* wb = win + (s & 1) * WINB;
 #pragma unroll 1
-    for (int pp = tid; pp < npv; pp += 256) {
-      if (bh == 16) bmv_vsum16<LP>(wb, pp, plane + pp);
-      else bmv_vsum_hb<LP>(wb, pp, bh, plane + pp);
+    for (int pp = tid; pp < npv; pp += NT) {
+      if (bh0 == 16) bmv_vsum16<LP>(wb, pp, plane + pp);
+      else bmv_vsum_hb<LP>(wb, pp, bh0, plane + pp);
+      if (two) bmv_vsum_hb<LP>(wb, pp, row_bh(1), plane2 + pp);
     }
     __syncthreads();
     typedef int i32x4 __attribute__((ext_vector_type(4)));
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-    constexpr int QB = 64;       // 4-position groups per plane row (256 positions)
-    i32x4 o[4];
+    constexpr int QB = 64;            // 4-position groups per plane row (256 positions)
+    constexpr int TPL = 1024 / NT;    // tasks per lane: 16 rows x 64 groups
+    i32x4 o[TPL], o2[TPL];
     const int nq = npos >> 2;
 #pragma unroll
-    for (int t = 0; t < 4; t++) {  // 16 rows x 64 groups = 1,024 tasks, 4 per lane
-      const int task = tid + 256 * t, k = task / QB, q = task - k * QB;
+    for (int t = 0; t < TPL; t++) {
+      const int task = tid + NT * t, k = task / QB, q = task - k * QB;
       if (q < nq) {
         const i32x4* vr = reinterpret_cast<const i32x4*>(plane + k * BMV_NP + 4 * q);
-        const i32x4 v0 = vr[0], v1 = vr[1], v2 = vr[2], v3 = vr[3];
-        o[t] = v0 + v1 + v2 + v3;
+        o[t] = vr[0] + vr[1] + vr[2] + vr[3];
+        if (two) {
+          const i32x4* v2 = reinterpret_cast<const i32x4*>(plane2 + k * BMV_NP + 4 * q);
+          o2[t] = v2[0] + v2[1] + v2[2] + v2[3];
+        }
       }
     }
     // the window's bytes become r' = r ^ 0x80 (the MFMA B operand)
-    for (int d = tid; d < WINB / 16; d += 256) {
+    for (int d = tid; d < WINB / 16; d += NT) {
       u32x4* w4 = reinterpret_cast<u32x4*>(wb) + d;
       *w4 = *w4 ^ 0x80808080u;
     }
     __syncthreads();
 #pragma unroll
-    for (int t = 0; t < 4; t++) {
-      const int task = tid + 256 * t, k = task / QB, q = task - k * QB;
-      if (q < nq) *reinterpret_cast<i32x4*>(plane + k * BMV_NP + 4 * q) = o[t];
+    for (int t = 0; t < TPL; t++) {
+      const int task = tid + NT * t, k = task / QB, q = task - k * QB;
+      if (q < nq) {
+        *reinterpret_cast<i32x4*>(plane + k * BMV_NP + 4 * q) = o[t];
+        if (two) *reinterpret_cast<i32x4*>(plane2 + k * BMV_NP + 4 * q) = o2[t];
+      }
     }
     __syncthreads();
   };
 
   MS_STAMP(0, __builtin_amdgcn_s_memtime());
   MS_STAMP(6, __builtin_amdgcn_s_memrealtime());
-  if (tid < 8) {
+  if (tid < 8 * R) {
     keys[tid] = ~0ull;
     cc[tid] = 0;
   }
   stage_band(0);
   __syncthreads();  // keys / cc initialised
-  if (tid < 128) {  // cur row records (c ^ 0x7F) and Cc = sum(c''^2 + 2 c'')
-    const int j = tid >> 4, rho = tid & 15;
+  if (tid < 128 * R) {  // cur row records (c ^ 0x7F) and Cc = sum(c''^2 + 2 c'')
+    const int jj = tid >> 4, rho = tid & 15, r = jj >> 3, j = jj & 7;
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     u32x4 v = {0u, 0u, 0u, 0u};
-    if (j < nb && rho < bh) {
+    if (r < nrw && j < nb && rho < row_bh(r)) {
       const u32x4* src = reinterpret_cast<const u32x4*>(
-          p.cur + (ptrdiff_t)(by + rho - p.cur_row0) * p.stride + 16 * (bc0 + j));
+          p.cur + (ptrdiff_t)(16 * (br0 + r) + rho - p.cur_row0) * p.stride + 16 * (bc0 + j));
       v = *src ^ 0x7F7F7F7Fu;
     }
     const u32x4 z = {0u, 0u, 0u, 0u};
-    u32x4* rec = reinterpret_cast<u32x4*>(crec + (16 * j + rho) * BM_CREC);
+    u32x4* rec = reinterpret_cast<u32x4*>(crec + (16 * jj + rho) * BM_CREC);
     rec[0] = z;
     rec[1] = v;
     rec[2] = z;
@@ -1446,13 +1480,16 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_bmv_kernel(SearchArgs p, Mf
       part = __builtin_amdgcn_sdot4((int)v[e], (int)v[e], part, false);
       part = __builtin_amdgcn_sdot4((int)v[e], 0x02020202, part, false);
     }
-    if (j < nb) atomicAdd(&cc[j], part);
+    if (r < nrw && j < nb) atomicAdd(&cc[jj], part);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  const int j0 = 2 * wave, j1 = j0 + 1;
-  const bool hasA = j0 < nb, hasB = j1 < nb;
+  const bool rowok = rw < nrw;
+  const int br = br0 + rw, by = 16 * br;
+  const int rylo = rowok ? row_ylo(rw) : 0, ryhi = rowok ? row_yhi(rw) : -1;
+  const int j0 = 2 * wl, j1 = j0 + 1;
+  const bool hasA = rowok && j0 < nb, hasB = rowok && j1 < nb;
   const int bxA = 16 * (bc0 + j0), bxB = bxA + 16;
   const int xloA = max(bxA - S, 0), xhiA = min(bxA + S, W - 16);
   const int xloB = max(bxB - S, 0), xhiB = min(bxB + S, W - 16);
@@ -1469,7 +1506,7 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_bmv_kernel(SearchArgs p, Mf
     for (int q = 0; q < 8; q++) {
 #pragma unroll
       for (int bsel = 0; bsel < 2; bsel++) {
-        const uint32_t a0 = lb + (uint32_t)(((2 * wave + bsel) * 16 + 2 * q) * BM_CREC);
+        const uint32_t a0 = lb + (uint32_t)(((8 * rw + 2 * wl + bsel) * 16 + 2 * q) * BM_CREC);
         uint32_t d[5];
 #pragma unroll
         for (int e = 0; e < 5; e++) d[e] = *reinterpret_cast<lds_c32*>((uintptr_t)(a0 + 4 * e));
@@ -1497,11 +1534,11 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_bmv_kernel(SearchArgs p, Mf
     xmask(2, i0B, xloB, xhiB);
     xmask(3, i1B, xloB, xhiB);
   }
-  const uint32_t ym = (!yover && n > yhi - ylo) ? 0x80000000u : 0u;
-  const bool fast = hasB && yover && bxA - S >= 0 && bxB + S <= W - 16 && i1A - i0A >= 2;
+  // interior pair in x: the mask-free tile sequence (y masks per band below)
+  const bool fastx = hasB && bxA - S >= 0 && bxB + S <= W - 16 && i1A - i0A >= 2;
   const int mfa = (bxA - S) & 15, mlb = (bxA + S) & 15;
-  // S2 of lane (n, h) at tile i: plane row n, positions 16 (i - tc0) + 4 h ..
-  const uint32_t s2base = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) int*)plane) +
+  int* splane = (two && rw == 1) ? plane2 : plane;
+  const uint32_t s2base = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) int*)splane) +
                           (uint32_t)((n * BMV_NP + 4 * h - 16 * tc0) * 4);
   const uint32_t lbase = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) uint8_t*)win) +
                          (uint32_t)((n + (h >> 1)) * LP + 16 * (h & 1) - 16 * tc0);
@@ -1509,13 +1546,16 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_bmv_kernel(SearchArgs p, Mf
   const v4i zero4 = {0, 0, 0, 0};
 
   unsigned long long bestA = ~0ull, bestB = ~0ull;
-  for (int s = 0; s < Ty; s++) {
-    if (s + 1 < Ty) stage_band(s + 1);
-    if (hasA) {
+  for (int s = 0; s < T; s++) {
+    if (s + 1 < T) stage_band(s + 1);
+    const int Ys = band_y(s);
+    if (hasA && Ys <= ryhi && Ys + 15 >= rylo) {
+      // rows of the band outside this block row's range: bit 31 of the key
+      const int yn = Ys + n;
+      const uint32_t ym = (yn < rylo || yn > ryhi) ? 0x80000000u : 0u;
+      const bool yfull = Ys >= rylo && Ys + 15 <= ryhi;
       const uint32_t lrow0 = lbase + (uint32_t)((s & 1) * WINB);
       uint32_t bA = ~0u, bB = ~0u;
-      // first / last tile masks, formed per band (not held across band_s2:
-      // opaque keeps the compiler from hoisting them out of the band loop)
       v4i mF, mL;
       const int h4b = opaque(4 * h);
 #pragma unroll
@@ -1533,9 +1573,10 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_bmv_kernel(SearchArgs p, Mf
         bA = ~0u;
         bB = ~0u;
       };
-      auto tile = [&](int i, auto DA, auto DB, auto MA, auto MB) {
+      auto tile = [&](int i, auto DA, auto DB, auto MA, auto MB, auto YM) {
         constexpr bool da = decltype(DA)::value, db = decltype(DB)::value;
         constexpr int ma = decltype(MA)::value, mb = decltype(MB)::value;
+        constexpr bool ymask = decltype(YM)::value;
         const v4i s2c = *reinterpret_cast<lds_v4i*>((uintptr_t)(s2base + (uint32_t)(64 * i)));
         const uint32_t lrow = (uint32_t)opaque((int)(lrow0 + (uint32_t)(16 * i)));
         v4i accA = ma == 1 ? mF : ma == 2 ? mL : zero4;
@@ -1578,7 +1619,7 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_bmv_kernel(SearchArgs p, Mf
           uint32_t k[4];
 #pragma unroll
           for (int r = 0; r < 4; r++) k[r] = ((uint32_t)acc[r] << 7) + P[r];
-          if constexpr (decltype(GEN)::value) {
+          if constexpr (ymask) {
 #pragma unroll
             for (int r = 0; r < 4; r++) k[r] |= ym;
           }
@@ -1595,45 +1636,49 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_bmv_kernel(SearchArgs p, Mf
       using M1 = std::integral_constant<int, 1>;
       using M2 = std::integral_constant<int, 2>;
       using M3 = std::integral_constant<int, 3>;
-      if (fast) {
-        tile(i0A, T_{}, F_{}, M1{}, M0{});
-        tile(i0A + 1, T_{}, T_{}, M0{}, M1{});
-        for (int i = i0A + 2; i < i1A; i++) tile(i, T_{}, T_{}, M0{}, M0{});
-        tile(i1A, T_{}, T_{}, M2{}, M0{});
-        tile(i1B, F_{}, T_{}, M0{}, M2{});
-      } else {
-        for (int i = iu0; i <= iu1; i++) {
-          const bool useA = i <= i1A, useB = hasB && i >= i0B;
-          if (useA && useB) tile(i, T_{}, T_{}, M3{}, M3{});
-          else if (useA) tile(i, T_{}, F_{}, M3{}, M3{});
-          else tile(i, F_{}, T_{}, M3{}, M3{});
+      auto seq = [&](auto YM) {
+        if (fastx) {
+          tile(i0A, T_{}, F_{}, M1{}, M0{}, YM);
+          tile(i0A + 1, T_{}, T_{}, M0{}, M1{}, YM);
+          for (int i = i0A + 2; i < i1A; i++) tile(i, T_{}, T_{}, M0{}, M0{}, YM);
+          tile(i1A, T_{}, T_{}, M2{}, M0{}, YM);
+          tile(i1B, F_{}, T_{}, M0{}, M2{}, YM);
+        } else {
+          for (int i = iu0; i <= iu1; i++) {
+            const bool useA = i <= i1A, useB = hasB && i >= i0B;
+            if (useA && useB) tile(i, T_{}, T_{}, M3{}, M3{}, T_{});
+            else if (useA) tile(i, T_{}, F_{}, M3{}, M3{}, T_{});
+            else tile(i, F_{}, T_{}, M3{}, M3{}, T_{});
+          }
         }
-      }
+      };
+      if (yfull) seq(F_{});
+      else seq(T_{});
       widen((iu1 - iu0) >> 4);
     }
     if (s == 0) MS_STAMP(2, __builtin_amdgcn_s_memtime());
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // band s + 1 landed (this thread's pieces)
     __syncthreads();                                   // ... and everyone's; band s and its S2 free
-    if (s + 1 < Ty) band_s2(s + 1);
+    if (s + 1 < T) band_s2(s + 1);
   }
   if (hasA) {
-    auto emit = [&](unsigned long long b, int j, int ccj, int bx) {
+    auto emit = [&](unsigned long long b, int j, int bx) {
       const uint32_t hi = (uint32_t)(b >> 32);
       if (hi < (1u << 25)) {
         const uint32_t lo = (uint32_t)b;
         const int sb = (int)(lo >> 8), seg = (int)((lo >> 6) & 3u), idx = (int)(lo & 63u);
-        const uint32_t cost = hi - 1u - (1u << 23) + (uint32_t)ccj;
+        const uint32_t cost = hi - 1u - (1u << 23) + (uint32_t)cc[8 * rw + j];
         const int dx = 16 * (iu0 + 16 * seg + (idx >> 2)) + 4 * h + (idx & 3) - bx;
         const int dy = band_y(sb) + n - by;
         const unsigned long long key = ((unsigned long long)cost << 32) |
                                        ((uint32_t)(dy + 32768) << 16) | (uint32_t)(dx + 32768);
         const uint32_t a = (uint32_t)(uintptr_t)(
-            (__attribute__((address_space(3))) unsigned long long*)(keys + j));
+            (__attribute__((address_space(3))) unsigned long long*)(keys + 8 * rw + j));
         asm volatile("ds_min_u64 %0, %1" : : "v"(a), "v"(key) : "memory");
       }
     };
-    emit(bestA, j0, cc[j0], bxA);
-    if (hasB) emit(bestB, j1, cc[j1], bxB);
+    emit(bestA, j0, bxA);
+    if (hasB) emit(bestB, j1, bxB);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
   __syncthreads();
@@ -1648,12 +1693,15 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_bmv_kernel(SearchArgs p, Mf
     g_mstamps[8 * blockIdx.x + 7] = __builtin_amdgcn_s_memrealtime();
   }
 #endif
-  if (tid < nb) {
-    const unsigned long long kk = keys[tid];
-    const int out = (br - p.block_row_begin) * p.nbx + bc0 + tid;
-    p.mv[2 * out] = (int16_t)((int)(kk & 0xFFFF) - 32768);
-    p.mv[2 * out + 1] = (int16_t)((int)((kk >> 16) & 0xFFFF) - 32768);
-    if (p.cost) p.cost[out] = (uint32_t)(kk >> 32);
+  if (tid < 8 * R) {
+    const int r = tid >> 3, j = tid & 7;
+    if (r < nrw && j < nb) {
+      const unsigned long long kk = keys[tid];
+      const int out = (br0 + r - p.block_row_begin) * p.nbx + bc0 + j;
+      p.mv[2 * out] = (int16_t)((int)(kk & 0xFFFF) - 32768);
+      p.mv[2 * out + 1] = (int16_t)((int)((kk >> 16) & 0xFFFF) - 32768);
+      if (p.cost) p.cost[out] = (uint32_t)(kk >> 32);
+    }
   }
 }
 
@@ -1741,7 +1789,9 @@ bool plan_mfma_ssd(const SearchArgs& p, MfmaGeom* g) {
   // no prepass planes (ME_MFMA_S2K=0|1 overrides; tuning build)
   const int s2k = tuning().mfma_s2k >= 0 ? tuning().mfma_s2k : kernel_path() == 3;
   g->bmv = g->bm && g->bm_lp == BMV_LP && s2k;
-  if (g->bmv) g->lds = BMV_LDS;
+  // block rows per workgroup (ME_MFMA_S2R=1|2 overrides; tuning build)
+  g->bmv_r = tuning().mfma_s2r > 0 ? tuning().mfma_s2r : 2;
+  if (g->bmv) g->lds = g->bmv_r == 2 ? bmv_lds<2>() : bmv_lds<1>();
   g->mkeys = p.mkeys;
   g->mcnt = p.mcnt;
   g->ya0 = max(r0 * 16 - S, 0);
@@ -1796,6 +1846,7 @@ static bool plan_mfma_ssd8(const SearchArgs& p, MfmaGeom* g) {
   g->hb_row = -1;
   g->bm = 0;
   g->bmv = 0;
+  g->bmv_r = 1;
   g->nbx = W / 8;
   g->tiles_x = (g->nbx + 3) / 4;
   g->tiles_y = (g->nrows + 3) / 4;
@@ -1827,11 +1878,17 @@ static bool plan_mfma_ssd8(const SearchArgs& p, MfmaGeom* g) {
   return true;
 }
 
+// Main-kernel workgroups per job: a block row each, or R rows each on the
+// lean path (me_mfma_bmv_kernel<R>).
+static int wgs_per_job(const MfmaGeom& g) {
+  return g.bmv ? (g.nrows + g.bmv_r - 1) / g.bmv_r * g.bm_wpr : g.nrows * g.bm_wpr;
+}
+
 // The one-job table of a single search (its own pointers, its own scratch).
 static MfmaJobs single_job(const SearchArgs& p, const MfmaGeom& g) {
   MfmaJobs jb;
   jb.n = 1;
-  jb.wgs = g.nrows * g.bm_wpr;
+  jb.wgs = wgs_per_job(g);
   jb.scratch_stride = 0;
   jb.ref[0] = p.ref;
   jb.cur[0] = p.cur;
@@ -1865,8 +1922,12 @@ static hipError_t launch_bm16(const SearchArgs& p, const MfmaGeom& g, const Mfma
 
 static hipError_t launch_bmv(const SearchArgs& p, const MfmaGeom& g, const MfmaJobs& jb,
                              hipStream_t stream) {
-  hipLaunchKernelGGL(me_mfma_bmv_kernel, dim3((unsigned)(jb.n * jb.wgs)), dim3(256), g.lds, stream,
-                     p, g, jb);
+  if (g.bmv_r == 2)
+    hipLaunchKernelGGL(me_mfma_bmv_kernel<2>, dim3((unsigned)(jb.n * jb.wgs)), dim3(512), g.lds,
+                       stream, p, g, jb);
+  else
+    hipLaunchKernelGGL(me_mfma_bmv_kernel<1>, dim3((unsigned)(jb.n * jb.wgs)), dim3(256), g.lds,
+                       stream, p, g, jb);
   return hipGetLastError();
 }
 
@@ -1954,7 +2015,7 @@ bool launch_mfma_jobs(const SearchArgs& base, const SearchJob* jobs, int n, hipS
   for (int i0 = 0; i0 < n && *err == hipSuccess; i0 += m) {
     MfmaJobs jb;
     jb.n = n - i0 < m ? n - i0 : m;
-    jb.wgs = g.nrows * g.bm_wpr;
+    jb.wgs = wgs_per_job(g);
     jb.scratch_stride = stride;
     for (int j = 0; j < jb.n; j++) {
       const SearchJob& J = jobs[i0 + j];
