@@ -1789,8 +1789,13 @@ bool plan_mfma_ssd(const SearchArgs& p, MfmaGeom* g) {
   // no prepass planes (ME_MFMA_S2K=0|1 overrides; tuning build)
   const int s2k = tuning().mfma_s2k >= 0 ? tuning().mfma_s2k : kernel_path() == 3;
   g->bmv = g->bm && g->bm_lp == BMV_LP && s2k;
-  // block rows per workgroup (ME_MFMA_S2R=1|2 overrides; tuning build)
-  g->bmv_r = tuning().mfma_s2r > 0 ? tuning().mfma_s2r : 2;
+  // block rows per workgroup (ME_MFMA_S2R=1|2 overrides; tuning build).  Two
+  // rows share each band's S2 (6 bands for two rows at S = 32 instead of
+  // 5 + 5; 10 instead of 9 + 9 at S = 64) but synchronise 8 waves per barrier
+  // and leave a row idle in the other row's end bands: 16-frame batches, 1080p
+  // +-32 35.9 us per frame against 33.8 with one row, 4K +-64 289 against 323
+  // (profiles/r04f_ssd_ab.jsonl).  Two rows from S = 48 on.
+  g->bmv_r = tuning().mfma_s2r > 0 ? tuning().mfma_s2r : (S >= 48 ? 2 : 1);
   if (g->bmv) g->lds = g->bmv_r == 2 ? bmv_lds<2>() : bmv_lds<1>();
   g->mkeys = p.mkeys;
   g->mcnt = p.mcnt;

@@ -30,7 +30,7 @@ struct Tuning {
   int flow_one = -1;      // ME_FLOW_ONE=0|1: a batch's flow jobs in launches of one ring / in one launch (-1 = automatic: one)
   int mfma_s2k = -1;      // ME_MFMA_S2K=0|1: 16x16 SSD, S <= 64: S2 from the prepass plane / formed in
                           // the workgroup (-1 = automatic: the kernel path, ME_PATH_MFMA_LEAN)
-  int mfma_s2r = 0;       // ME_MFMA_S2R=1|2: lean path block rows per workgroup (0 = automatic: 2)
+  int mfma_s2r = 0;       // ME_MFMA_S2R=1|2: lean path block rows per workgroup (0 = automatic: 2 from S = 48)
   int mfma_batch = -1;    // ME_MFMA_BATCH=0|1: equal SSD jobs share matrix-core launches (-1 = automatic: on)
   int strip = -1;         // ME_STRIP=0..64: item-kernel tile strips (0 = row-major; -1 = automatic)
 };
