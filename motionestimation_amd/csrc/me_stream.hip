@@ -7,10 +7,9 @@
 // pairs of frames/ForemanYF{1,2,4}) -- and keeps every device busy:
 //   - each frame is uploaded once per device, into a device slot that lives
 //     from the first to the last pair reading it;
-//   - pairs are searched 4 at a time in one job-table launch (launch_jobs),
-//     which pays a launch's fill and drain once per 4 pairs: CIF pan 30.3k ->
-//     38.4k pairs/s; 1080p stays bound by the upload (~22 GB/s H2D), 10.8k ->
-//     11.0k (profiles/r03bn_stream_batch_sweep.txt);
+//   - pairs are searched in job-table launches (launch_jobs) of 1, 2, 4 and
+//     then 8 pairs: a launch's fill and drain are paid once per batch, and
+//     the first search starts after two uploads (profiles/r04h_*);
 //   - uploads run on a copy stream, searches on the compute stream; the
 //     host-side staging and upload of pair n+1's new frame overlap the search
 //     of pair n (slots are reused oldest-freed first, so an upload never
@@ -45,7 +44,7 @@ std::map<uintptr_t, size_t> g_pinned;  // me_host_alloc ranges: base -> bytes
 // Freed frame slots kept cooling before reuse (ME_STREAM_COOL overrides; tuning)
 static int cooling_slots() { return tuning().stream_cool > 0 ? tuning().stream_cool : 2; }
 // Pairs per search launch (ME_STREAM_BATCH overrides; tuning)
-constexpr int kPairBatch = 4;
+constexpr int kPairBatch = 8;
 constexpr int kEvRing = 16;  // batch events (Dev::upl_ev / batch_ev), ring by batch index
 }  // namespace
 
@@ -208,8 +207,11 @@ me_status run_pairs(me_ctx* c, Dev& d, const Job& j, int p0, int p1) {
   std::vector<SearchJob> jobs;
   jobs.reserve((size_t)G);
   int batch = 0;
-  for (int n0 = p0; n0 < p1; n0 += G, batch++) {
-    const int n1 = std::min(p1, n0 + G);
+  // Batches ramp up 1, 2, 4, ... G pairs: the first search starts after two
+  // uploads instead of G + 1, and the next batch's uploads overlap it.
+  for (int n0 = p0, gb = 1; n0 < p1; n0 += gb, gb = std::min(2 * gb, G), batch++) {
+    if (tuning().stream_batch > 0) gb = G;  // tuning build: fixed batches (the round-3 behaviour)
+    const int n1 = std::min(p1, n0 + gb);
     if (kAhead <= 8 && batch >= kAhead) {
       HIPCHK(c, hipEventSynchronize(d.batch_ev[(batch - kAhead) % kEvRing]));
       synced = batch - kAhead;

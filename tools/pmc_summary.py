@@ -5,6 +5,12 @@ HBM bytes per launch follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE
 are in KiB (x1024); on gfx950 FETCH_SIZE reports exactly half the bytes of a
 wide coalesced (16 B/lane) streaming read, so it is doubled; WRITE_SIZE is
 exact for such stores.  The counters come from separate passes.
+
+bench.py launches a kernel at more than one size in one run (the timed F-frame
+batch, then F one-frame parity calls on the same persistent grid), so every
+per-launch figure (time, FETCH, WRITE) is taken over the kernel's *batch*
+launches only: dispatches lasting at least half the kernel's longest one in
+that pass.  The one-frame launches are reported beside them ("single").
 """
 import csv
 import glob
@@ -39,6 +45,17 @@ def is_me(name):
     return "me_" in name or "qsad" in name or "generic" in name
 
 
+def split(per):
+    """{kernel: [(duration_ns, value)]} -> {kernel: (batch mean, single mean or None, n batch)}"""
+    out = {}
+    for k, v in per.items():
+        top = max(d for d, _ in v)
+        big = [x for d, x in v if d >= 0.5 * top]
+        small = [x for d, x in v if d < 0.5 * top]
+        out[k] = (sum(big) / len(big), sum(small) / len(small) if small else None, len(big))
+    return out
+
+
 def counter(pattern, cname):
     rs, _ = rows(pattern)
     per = {}
@@ -46,12 +63,28 @@ def counter(pattern, cname):
         name = r.get("Kernel_Name") or r.get("Kernel-Name") or ""
         if r.get("Counter_Name") != cname or not is_me(name):
             continue
-        per.setdefault(name, []).append(float(r["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in per.items()}
+        dur = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        per.setdefault(name, []).append((dur, float(r["Counter_Value"])))
+    return split(per)
+
+
+def trace_times():
+    per = {}
+    for r in ktrace:
+        name = r.get("Kernel_Name", "")
+        if is_me(name):
+            dur = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+            per.setdefault(name, []).append((dur, float(dur)))
+    return split(per)
 
 
 fetch = counter("*counter_collection.csv", "FETCH_SIZE")
 write = counter("*counter_collection.csv", "WRITE_SIZE")
+times = trace_times()
+# optional passes (profile.sh SIZED=1): read requests by size, L2 hits / misses
+sized = {c: counter("*counter_collection.csv", c) for c in
+         ("TCC_EA0_RDREQ_32B_sum", "TCC_EA0_RDREQ_64B_sum", "TCC_EA0_RDREQ_128B_sum",
+          "TCC_EA0_RDREQ_sum", "TCC_HIT_sum", "TCC_MISS_sum")}
 summary = {}
 for r in stats:
     name = r.get("Name", "")
@@ -59,21 +92,34 @@ for r in stats:
         continue
     summary[name] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
                      "min_ns": float(r["MinNs"]), "max_ns": float(r["MaxNs"])}
-for name, v in fetch.items():
-    summary.setdefault(name, {})["fetch_kib"] = v
-for name, v in write.items():
-    summary.setdefault(name, {})["write_kib"] = v
+for name, (big, small, n) in times.items():
+    e = summary.setdefault(name, {})
+    e.update({"batch_calls": n, "batch_avg_ns": big, "single_avg_ns": small})
+for name, (big, small, _) in fetch.items():
+    summary.setdefault(name, {}).update({"fetch_kib": big, "single_fetch_kib": small})
+for name, (big, small, _) in write.items():
+    summary.setdefault(name, {}).update({"write_kib": big, "single_write_kib": small})
 dom = max(summary, key=lambda k: summary[k].get("avg_ns", 0) * summary[k].get("calls", 0))
 d = summary[dom]
-hbm = None
+for c, per in sized.items():
+    for name, (big, small, _) in per.items():
+        summary.setdefault(name, {}).update({c: big, "single_" + c: small})
+hbm = hbm_single = None
 if "fetch_kib" in d and "write_kib" in d:
     hbm = 2 * d["fetch_kib"] * 1024 + d["write_kib"] * 1024
+    if d.get("single_fetch_kib") is not None and d.get("single_write_kib") is not None:
+        hbm_single = 2 * d["single_fetch_kib"] * 1024 + d["single_write_kib"] * 1024
+# read bytes from the request sizes, where that pass ran
+rd_sized = None
+if all(k in d for k in ("TCC_EA0_RDREQ_32B_sum", "TCC_EA0_RDREQ_64B_sum", "TCC_EA0_RDREQ_128B_sum")):
+    rd_sized = (32 * d["TCC_EA0_RDREQ_32B_sum"] + 64 * d["TCC_EA0_RDREQ_64B_sum"] +
+                128 * d["TCC_EA0_RDREQ_128B_sum"])
 # every kernel of one search (the SSD prepass beside its main kernel): bytes per
 # launch of each, weighted by its launches per dominant-kernel launch
 search = 0.0
 for k, v in summary.items():
     if "fetch_kib" in v and "write_kib" in v and v.get("calls"):
-        per = v["calls"] / max(d.get("calls", 1), 1)
+        per = v.get("batch_calls", v["calls"]) / max(d.get("batch_calls", d.get("calls", 1)), 1)
         search += per * (2 * v["fetch_kib"] * 1024 + v["write_kib"] * 1024)
 bench_tag = None
 cfg = "1080p"
@@ -100,9 +146,12 @@ except (OSError, ValueError):
     allsum = {}
 allsum[bench_tag] = {"profile_tag": tag, "dominant_kernel": dom, "kernels": summary,
                      "hbm_bytes_per_launch": hbm,
+                     "hbm_bytes_per_single_frame_launch": hbm_single,
+                     "read_bytes_by_request_size": rd_sized,
                      "hbm_bytes_per_search": search or None,
                      "note": "hbm = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 correction, "
                              "MI355X_MICROARCH.md §HBM); separate --pmc passes; per_launch: the "
-                             "dominant kernel; per_search: every kernel of one search"}
+                             "dominant kernel's batch launches (>= half its longest); "
+                             "per_search: every kernel of one search"}
 json.dump(allsum, open(path, "w"), indent=1)
 print(json.dumps(allsum[bench_tag], indent=1))

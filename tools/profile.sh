@@ -4,6 +4,9 @@
 # 1) rocprofv3 --kernel-trace --stats  (per-kernel durations)
 # 2) rocprofv3 --pmc FETCH_SIZE        (own pass: TCC slots, MI355X_MICROARCH.md)
 # 3) rocprofv3 --pmc WRITE_SIZE        (own pass)
+# 4) SIZED=1: the L2's fabric read requests by size (32/64/128 B) and the L2
+#    hit/miss counts, two more passes (FETCH_SIZE is requests x 64 B, so the
+#    doubling of MI355X_MICROARCH.md holds only if every request is 128 B)
 # then tools/pmc_summary.py folds them into profiles/pmc_summary.json and
 # copies the stats CSVs to profiles/<tag>_*.
 set -o pipefail
@@ -16,5 +19,9 @@ export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -d "$OUT/kt" -o run --output-format csv -- python3 bench.py $ARGS > "$OUT/kt.log" 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -T -d "$OUT/fetch" -o run --output-format csv -- python3 bench.py $ARGS > "$OUT/fetch.log" 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -T -d "$OUT/write" -o run --output-format csv -- python3 bench.py $ARGS > "$OUT/write.log" 2>&1 || exit $?
+if [ "${SIZED:-0}" = 1 ]; then
+  timeout -k 10 300 rocprofv3 --pmc TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_sum -T -d "$OUT/rdreq" -o run --output-format csv -- python3 bench.py $ARGS > "$OUT/rdreq.log" 2>&1 || exit $?
+  timeout -k 10 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -T -d "$OUT/hit" -o run --output-format csv -- python3 bench.py $ARGS > "$OUT/hit.log" 2>&1 || exit $?
+fi
 find "$OUT" -name "*.csv" | head -50
 python3 tools/pmc_summary.py "$OUT" "$TAG" $ARGS
