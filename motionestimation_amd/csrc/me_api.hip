@@ -67,6 +67,8 @@ static Tuning read_tuning() {
   env_int("ME_FLOW_SLOTS", 2, 16, &t.flow_slots);
   env_int("ME_PRIO", 0, 1, &t.prio);
   env_int("ME_STRIP", 0, 64, &t.strip);
+  env_int("ME_AHEAD", 1, 2, &t.ahead);
+  env_int("ME_ITEM_BATCH", 0, 1, &t.item_batch);
   env_int("ME_FAIR", 0, 3, &t.fair);
   env_int("ME_FLOW_ONE", 0, 1, &t.flow_one);
   env_int("ME_MFMA_BATCH", 0, 1, &t.mfma_batch);
@@ -256,7 +258,7 @@ me_status launch_ordered(me_ctx* c, Dev& d, SearchArgs& p, hipStream_t s) {
   const hipError_t e = launch_search(p, s, nullptr);
   if (e != hipSuccess) {
     if (!cap) {
-      (void)hipMemsetAsync(d.sched, 0, 64, s);
+      (void)hipMemsetAsync(d.sched, 0, SCHED_WORDS * 4, s);
       if (d.mkeys) (void)hipMemsetAsync(d.mkeys, 0xFF, d.merge_cap * 16 * 8, s);
       if (d.mcnt) (void)hipMemsetAsync(d.mcnt, 0, d.merge_cap * 4, s);
     }
@@ -274,7 +276,7 @@ me_status launch_jobs_ordered(me_ctx* c, Dev& d, const SearchArgs& base, const S
   const hipError_t e = launch_jobs(base, jobs, n, s);
   if (e != hipSuccess) {
     if (!cap) {
-      (void)hipMemsetAsync(d.sched, 0, 64, s);
+      (void)hipMemsetAsync(d.sched, 0, SCHED_WORDS * 4, s);
       if (d.mkeys) (void)hipMemsetAsync(d.mkeys, 0xFF, d.merge_cap * 16 * 8, s);
       if (d.mcnt) (void)hipMemsetAsync(d.mcnt, 0, d.merge_cap * 4, s);
     }
@@ -587,7 +589,8 @@ me_status me_create(me_ctx** out, const int* device_ids, int n) {
     d.id = id;
     if (hipSetDevice(id) != hipSuccess ||
         hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc((void**)&d.sched, 64) != hipSuccess || hipMemset(d.sched, 0, 64) != hipSuccess ||
+        hipMalloc((void**)&d.sched, me::SCHED_WORDS * 4) != hipSuccess ||
+        hipMemset(d.sched, 0, me::SCHED_WORDS * 4) != hipSuccess ||
         hipEventCreateWithFlags(&d.search_ev, hipEventDisableTiming) != hipSuccess) {
       c->devs.push_back(d);
       me_destroy(c);

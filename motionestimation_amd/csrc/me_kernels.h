@@ -11,9 +11,14 @@ enum { COST_SSD = 0, COST_SAD = 1, COST_SSIM = 2 };
 constexpr int GENERIC_THREADS = 256;
 constexpr int GENERIC_LDS_BUDGET = 60 * 1024;
 constexpr int QSAD_LDS_BUDGET = 40 * 1024;  // 4 workgroups per CU (160 KB LDS)
-// sched[SCHED_ERR]: a kernel whose bounded wait expired sets it (the host
-// reads and clears it: device_status, me_device_check).  sched holds 16 u32.
-constexpr int SCHED_ERR = 15;
+// sched holds SCHED_WORDS u32: [0, 16) the item kernel's 8 two-ended band
+// counters (u64: owner claims in the low half, thieves in the high half),
+// [SCHED_ARRIVE] its arrivals (the last workgroup out re-zeroes [0, 17)),
+// [SCHED_ERR]: a kernel whose bounded wait expired sets it (the host reads and
+// clears it: device_status, me_device_check).
+constexpr int SCHED_WORDS = 32;
+constexpr int SCHED_ARRIVE = 16;
+constexpr int SCHED_ERR = 31;
 
 // One search launch: block rows [block_row_begin, block_row_end) of a
 // width x height frame.  ref / cur point at frame rows ref_row0 / cur_row0.
@@ -31,8 +36,7 @@ struct SearchArgs {
   uint32_t* cost;
   uint32_t ref_bytes;  // readable bytes from ref (buffer range check), and from cur
   uint32_t cur_bytes;
-  uint32_t* sched;     // 16 u32: [0, 9) zeroed tile counters + arrivals (8 XCD groups),
-                       // [SCHED_ERR] the invariant word; or null
+  uint32_t* sched;     // SCHED_WORDS u32 (layout above), zeroed between launches; or null
   uint8_t* scratch;    // device scratch of the MFMA SSD path (mfma_ssd_scratch bytes) or null
   size_t scratch_bytes;
   // MFMA SSD cross-workgroup merge (self-resetting): 16 keys (~0) per tile and
@@ -66,6 +70,7 @@ struct QsadGeom {
   int fold;        // SAD, S % 4 == 0: groups = S/2 cover dx in [-S, S-1]; the dx = +S
                    // column is spread over lanes gi < K, one v_sad_u8 candidate each
   int dyn_tiles;   // dynamic tile pulls when tiles >= dyn_tiles * workgroups (0: never)
+  int pull_ahead;  // dynamic: tile ti + pull_ahead is claimed when tile ti starts (1 or 2)
   int flow_slots;  // me_flow_kernel: LDS ring slots (0: the persistent item kernel)
   int prio;        // waves issuing staging raise their issue priority (s_setprio) meanwhile
   int fair;        // me_flow_kernel: lo | hi << 8 | mode << 16 (0: off): a wave whose

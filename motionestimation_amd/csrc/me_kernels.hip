@@ -654,19 +654,28 @@ __global__ __launch_bounds__(1024) void me_fast_kernel(SearchArgs p, QsadGeom g,
   // profiles/r03c_wave_stamps.txt).
   if (g.prio) __builtin_amdgcn_s_setprio(3);
   // Dynamic: each workgroup's first two tiles are its static ones (no atomic
-  // storm at launch); the counter of band y hands out the band's tiles past
-  // its first 2 * n_y.  Own band first; once it is exhausted, steal from the
-  // other XCD groups' bands (clocks differ by several % between XCDs, so
-  // bands finish unevenly).
+  // storm at launch); band y's tiles past its first 2 * n_y are claimed from a
+  // two-ended u64 counter: its own workgroups from the front (low half), once
+  // their band is exhausted other XCD groups' workgroups from the back (high
+  // half; clocks differ by several % between XCDs, so bands finish unevenly).
+  // One atomic add per claim and the claim is valid iff lo + hi < avail of the
+  // returned old value, so every tile is claimed once.  Thieves take the band's
+  // LAST rows, contiguously, where front steals each re-read a whole window
+  // (2S + B rows) on the thief's XCD for B rows of output; at 4K +-64 steals
+  // are few and both measured alike (365 vs 368 MB per 16-frame launch,
+  // profiles/r04i_*, r04j_*: the excess there was the claim distance, below).
   auto pull = [&]() -> int {
     for (int d = 0; d < ng; d++) {
       const int y = x + d < ng ? x + d : x + d - ng;
       const int b0 = (int)((long)ntiles * y / ng), b1 = (int)((long)ntiles * (y + 1) / ng);
       const int n_y = nwg / ng + (y < nwg % ng ? 1 : 0);
-      const int first = min(b1 - b0, 2 * n_y);
-      const uint32_t i = __hip_atomic_fetch_add(p.sched + y, 1u, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-      if ((int)i < b1 - b0 - first) return b0 + first + (int)i;
+      const int first = min(b1 - b0, 2 * n_y), avail = b1 - b0 - first;
+      if (avail <= 0) continue;
+      const uint64_t o = __hip_atomic_fetch_add(reinterpret_cast<uint64_t*>(p.sched) + y,
+                                                d == 0 ? 1ull : (1ull << 32), __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+      const int lo = (int)(uint32_t)o, hi = (int)(o >> 32);
+      if (lo + hi < avail) return d == 0 ? b0 + first + lo : b1 - 1 - hi;
     }
     return -1;
   };
@@ -677,11 +686,17 @@ __global__ __launch_bounds__(1024) void me_fast_kernel(SearchArgs p, QsadGeom g,
   auto tile_at = [&](int i) -> int {  // i-th tile of this workgroup, -1 = none
     return dyn ? tq[i & 3] : static_tile(i);
   };
+  auto claim = [&](int i) -> int {  // tile i of this workgroup (dynamic)
+    if (i < 2) {
+      const int t = static_tile(i);
+      if (t >= 0) return t;
+    }
+    return pull();
+  };
+  const int ahead = g.pull_ahead;
   if (dyn && tid == 0) {
-    tq[0] = static_tile(0);
-    if (tq[0] < 0) tq[0] = pull();
-    tq[1] = static_tile(1);
-    if (tq[1] < 0 && tq[0] >= 0) tq[1] = pull();
+    tq[0] = claim(0);
+    if (ahead == 2) tq[1] = tq[0] >= 0 ? claim(1) : -1;
   }
   if (tid < g.tb) keys[tid] = ~0ull;
   __syncthreads();
@@ -700,9 +715,9 @@ __global__ __launch_bounds__(1024) void me_fast_kernel(SearchArgs p, QsadGeom g,
     __syncthreads();  // item k staged by every wave; item k-1 fully consumed
     if (k == 0) ME_STAMP(2, __builtin_amdgcn_s_memtime());  // first item staged
     if (k == 0) ME_WSTAMP(1, __builtin_amdgcn_s_memtime());
-    if (dyn && pass == 0 && tid == 0) {  // starting tile ti: pull tile ti + 2
-      const int prev = tq[(ti + 1) & 3];
-      tq[(ti + 2) & 3] = prev >= 0 ? pull() : -1;
+    if (dyn && pass == 0 && tid == 0) {  // starting tile ti: claim tile ti + ahead
+      const int prev = tq[(ti + ahead - 1) & 3];
+      tq[(ti + ahead) & 3] = prev >= 0 ? claim(ti + ahead) : -1;
     }
     {
       const int ntile = pass + 1 < passes ? tile : tile_at(ti + 1);
@@ -863,12 +878,12 @@ __global__ __launch_bounds__(1024) void me_fast_kernel(SearchArgs p, QsadGeom g,
     // The last workgroup out re-zeroes the counters for the next launch on
     // this stream (every other workgroup's final pull precedes its arrival).
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    const uint32_t d = __hip_atomic_fetch_add(p.sched + 8, 1u, __ATOMIC_RELAXED,
+    const uint32_t d = __hip_atomic_fetch_add(p.sched + SCHED_ARRIVE, 1u, __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_AGENT);
     if (d == (uint32_t)nwg - 1) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 #pragma unroll
-      for (int i = 0; i < 9; i++)
+      for (int i = 0; i <= SCHED_ARRIVE; i++)
         __hip_atomic_store(p.sched + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
@@ -1443,6 +1458,14 @@ bool plan_fast(const SearchArgs& p, QsadGeom* g, int* k_out) {
   // (the row-major order fetched 2.4x the algorithmic bytes at 8K SAD).
   g->strip_w = g->wg_per_row >= 32 && rows >= 32 ? 16 : 0;
   if (tu.strip >= 0) g->strip_w = tu.strip;
+  // Dynamic pulls claim a workgroup's next tile when its current one starts if
+  // a tile has >= 2 passes (the id is read at the last pass, a barrier later),
+  // else two tiles ahead.  Claimed-but-unstarted tiles widen the band of rows
+  // an XCD's workgroups touch at once: ahead = 2 at 4K +-64 (128 workgroups
+  // per XCD, 3 passes) fetched 1.35x the compulsory bytes, ahead = 1
+  // 1.11x, at the same time (profiles/r04l_variants_4k.txt).
+  g->pull_ahead = (g->chunks + g->cpp - 1) / g->cpp >= 2 ? 1 : 2;
+  if (tu.ahead > 0 && (tu.ahead == 2 || g->pull_ahead == 1)) g->pull_ahead = tu.ahead;
   *k_out = bK;
   return true;
 }
@@ -1537,6 +1560,7 @@ bool plan_flow(const SearchArgs& p, QsadGeom* g) {
   q.tile16 = 1;
   q.threads = 1024;
   q.dyn_tiles = 0;
+  q.pull_ahead = 2;
   q.pitch_magic = (uint32_t)(0x100000000ull / (uint64_t)q.pitch) + 1u;
   for (uint32_t d = 0; d < (uint32_t)q.tile_bytes; d += 16)
     if ((uint32_t)(((uint64_t)d * q.pitch_magic) >> 32) != d / (uint32_t)q.pitch) return false;
@@ -1933,7 +1957,8 @@ static bool launch_item_jobs(const SearchArgs& base, const SearchJob* jobs, int 
     const long pos = (long)base.nbx * (jobs[i].r1 - jobs[i].r0) * win;
     max_pos = pos > max_pos ? pos : max_pos;
   }
-  const int per = max_pos >= (1L << 33) ? 1 : MAX_JOBS;
+  int per = max_pos >= (1L << 33) ? 1 : MAX_JOBS;
+  if (tuning().item_batch >= 0) per = tuning().item_batch ? MAX_JOBS : 1;
   for (int i0 = 0; i0 < n && *err == hipSuccess; i0 += per) {
     const int m = n - i0 < per ? n - i0 : per;
     SearchJob fj[MAX_JOBS];

@@ -48,6 +48,12 @@ hw = st[:, 4].astype(np.int64)
 xcc = st[:, 5].astype(np.int64) & 0xF
 simd = (hw >> 4) & 3
 cu = (xcc << 8) | (((hw >> 13) & 7) << 5) | (((hw >> 12) & 1) << 4) | ((hw >> 8) & 0xF)
+# workgroup -> XCD placement: the kernels assume blocks b and b + 8 share an
+# XCD (bands of tiles per b % 8); print which XCCs each residue landed on
+res = {}
+for g_, x_ in zip(idx // 4, xcc):
+    res.setdefault(int(g_) % 8, set()).add(int(x_))
+print("  XCC ids per workgroup index % 8:", {r: sorted(v) for r, v in sorted(res.items())})
 # per-XCD s_memtime base
 base = {x: st[xcc == x, 0].min() for x in np.unique(xcc)}
 b = np.array([base[x] for x in xcc], dtype=np.uint64)
