@@ -745,10 +745,8 @@ def stripe_record(eng, dev, world, rank, gloo, cfg_name, cost, steps, warmup, nf
 
 def sad_frames_per_launch(w, h, blk, span, F):
     """Frames per SAD launch of an F-frame batch: one launch of up to MAX_JOBS
-    frames, except frames of >= 2^33 window positions (blocks x (2S+1)^2: 8K
-    8x8 +-128), which launch one by one (me_kernels.hip launch_item_jobs)."""
-    nb = ((w + blk - 1) // blk) * ((h + blk - 1) // blk)
-    return 1 if nb * (2 * span + 1) ** 2 >= 1 << 33 else min(F, MAX_JOBS)
+    frames (me_kernels.hip launch_flow_jobs / launch_item_jobs), 8K included."""
+    return min(F, MAX_JOBS)
 
 
 def ssd_frames_per_launch(w, h, blk, span, F):
@@ -920,7 +918,7 @@ def main():
     # Stripe mode: the frame's work / N against the slowest rank's kernel time.
     # Priced per launch of the dominant kernel.  SAD batches share launches of
     # up to MAX_JOBS (32) frames (1080p: the flow kernel's job table; 4K: the
-    # item kernel's; 8K 8x8 frames launch one by one, sad_frames_per_launch); B = 16 SSD batches share a prepass and a block-major
+    # item kernel's, sad_frames_per_launch); B = 16 SSD batches share a prepass and a block-major
     # launch (ssd_frames_per_launch), 8x8 SSD launches per frame.
     # So a launch holds fpl frames and lasts kern_ms * fpl / F.  Stripe mode:
     # the rank's F stripes, one launch per step (F <= 32).  roofline.traffic is

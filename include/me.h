@@ -222,7 +222,8 @@ me_status me_gather_device(me_ctx* ctx, const void* d_send, size_t bytes, void* 
  * reported an error, or the wait timed out (a peer rank stalled or died); the
  * communicator is then aborted (ncclCommAbort), so this rank's RCCL kernels
  * return and the stream can be synchronised instead of hanging, and every
- * later me_gather_device / me_comm_check on the context fails with ME_ECOMM.
+ * later me_gather_device / me_comm_check on the context fails with ME_ECOMM
+ * until me_comm_init builds a new communicator (all ranks, a fresh id).
  * me_last_error names the cause.  The multi-device me_full_search waits the
  * same way (ME_COMM_TIMEOUT_MS) and rebuilds its group after a failure. */
 #define ME_COMM_TIMEOUT_MS 60000

@@ -630,6 +630,7 @@ me_status me_comm_init(me_ctx* c, const void* id, int n_ranks, int rank) {
   c->rank_comm = comm;
   c->comm_ranks = n_ranks;
   c->comm_rank = rank;
+  c->comm_aborted = false;  // a communicator rebuilt after me_comm_check aborted the last one
   return ME_OK;
 }
 

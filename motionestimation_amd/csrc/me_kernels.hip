@@ -1946,19 +1946,15 @@ static bool launch_item_jobs(const SearchArgs& base, const SearchJob* jobs, int 
   QsadGeom g;
   int K = 0;
   if (!cached_plan(probe, &g, &K)) return false;
-  // A job that alone fills the chip many times over (blocks x (2S+1)^2 >= 2^33
-  // window positions: 8K 8x8 +-128, 3.4e10, 2.5k items per CU) gains nothing
-  // from sharing a launch (8K: 17.19 vs 17.25 ms per frame) and costs L2
-  // reuse there (124 against 98 MB fetched per frame, profiles/r03aw_*): such
-  // jobs launch one by one (bench.py's item_frames_per_launch mirrors this).
-  const long win = (2L * base.range + 1) * (2L * base.range + 1);
-  long max_pos = 0;
-  for (int i = 0; i < n; i++) {
-    const long pos = (long)base.nbx * (jobs[i].r1 - jobs[i].r0) * win;
-    max_pos = pos > max_pos ? pos : max_pos;
-  }
-  int per = max_pos >= (1L << 33) ? 1 : MAX_JOBS;
-  if (tuning().item_batch >= 0) per = tuning().item_batch ? MAX_JOBS : 1;
+  // Every job shares the launch, however large: with whole frames per XCD band
+  // the bands need no halo rows.  8K 8x8 +-128, 16 frames: 17.09 ms and 70.7 MB
+  // read per frame in one row-major launch, against 17.26 ms and 89.9 MB one
+  // launch per frame (profiles/r04m_variants_8k.txt; round 3 measured the
+  // opposite, 124 vs 98 MB, with tiles claimed two ahead).  Row-major: the
+  // strip walk, which keeps a single wide frame's window rows in L2, only
+  // spreads a batch's working set (same run: strips of 16 tiles 87.9 MB).
+  const int per = tuning().item_batch == 0 ? 1 : MAX_JOBS;  // tuning build: ME_ITEM_BATCH=0
+  if (n > 1 && tuning().strip < 0) g.strip_w = 0;
   for (int i0 = 0; i0 < n && *err == hipSuccess; i0 += per) {
     const int m = n - i0 < per ? n - i0 : per;
     SearchJob fj[MAX_JOBS];

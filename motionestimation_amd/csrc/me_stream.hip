@@ -19,7 +19,9 @@
 //     launches delayed each launch by 58-74 us (profiles/r04e_*);
 //   - frames in me_host_alloc memory are DMAed directly, other frames are
 //     staged through two pinned buffers;
-//   - MV records stay in HBM until the run ends, then one copy per output.
+//   - each batch's MV records are downloaded (pinned bounce buffer, own stream)
+//     after its search and moved to the caller's arrays while later batches
+//     search: one copy at the end took 250 us of host time at 64 1080p pairs.
 // With several context devices the pair list is cut into contiguous runs,
 // one per device, each driven by its own host thread (independent pairs: no
 // collective).
@@ -59,12 +61,19 @@ bool host_range_pinned(const void* p, size_t bytes) {
 
 void release_pipeline(Dev& d) {
   if (d.copy) (void)hipStreamSynchronize(d.copy);
+  if (d.d2h) (void)hipStreamSynchronize(d.d2h);
   for (size_t i = 0; i < d.slots.size(); i++) (void)hipFree(d.slots[i]);
   for (int k = 0; k < kEvRing; k++) {
     if (d.upl_ev[k]) (void)hipEventDestroy(d.upl_ev[k]);
     if (d.batch_ev[k]) (void)hipEventDestroy(d.batch_ev[k]);
-    d.upl_ev[k] = d.batch_ev[k] = nullptr;
+    if (d.d2h_ev[k]) (void)hipEventDestroy(d.d2h_ev[k]);
+    d.upl_ev[k] = d.batch_ev[k] = d.d2h_ev[k] = nullptr;
   }
+  if (d.bounce) (void)hipHostFree(d.bounce);
+  d.bounce = nullptr;
+  d.bounce_cap = 0;
+  if (d.d2h) (void)hipStreamDestroy(d.d2h);
+  d.d2h = nullptr;
   d.slots.clear();
   d.slot_bytes = 0;
   for (int k = 0; k < 2; k++) {
@@ -101,10 +110,13 @@ me_status prepare(me_ctx* c, Dev& d, size_t plane) {
     d.slot_bytes = plane;
   }
   if (!d.copy) HIPCHK(c, hipStreamCreateWithFlags(&d.copy, hipStreamNonBlocking));
+  if (!d.d2h) HIPCHK(c, hipStreamCreateWithFlags(&d.d2h, hipStreamNonBlocking));
   for (int k = 0; k < kEvRing; k++) {
     if (!d.upl_ev[k]) HIPCHK(c, hipEventCreateWithFlags(&d.upl_ev[k], hipEventDisableTiming));
     if (!d.batch_ev[k]) HIPCHK(c, hipEventCreateWithFlags(&d.batch_ev[k], hipEventDisableTiming));
+    if (!d.d2h_ev[k]) HIPCHK(c, hipEventCreateWithFlags(&d.d2h_ev[k], hipEventDisableTiming));
   }
+  HIPCHK(c, hipStreamSynchronize(d.d2h));  // a failed earlier call may have left copies
   return ME_OK;
 }
 
@@ -161,6 +173,29 @@ me_status run_pairs(me_ctx* c, Dev& d, const Job& j, int p0, int p1) {
   if ((s = grow(c, (void**)&d.pair_out, &d.pair_out_cap, np * nb * 8)) != ME_OK) return s;
   int16_t* out_mv = reinterpret_cast<int16_t*>(d.pair_out);
   uint32_t* out_cost = reinterpret_cast<uint32_t*>(d.pair_out + np * nb * 4);
+  if (d.bounce_cap < np * nb * 8) {
+    if (d.bounce) (void)hipHostFree(d.bounce);
+    d.bounce = nullptr;
+    d.bounce_cap = 0;
+    if (hipHostMalloc((void**)&d.bounce, np * nb * 8, hipHostMallocDefault) != hipSuccess)
+      return fail(c, ME_ENOMEM, "pinned record buffer of %zu bytes failed", np * nb * 8);
+    d.bounce_cap = np * nb * 8;
+  }
+  int16_t* bnc_mv = reinterpret_cast<int16_t*>(d.bounce);
+  uint32_t* bnc_cost = reinterpret_cast<uint32_t*>(d.bounce + np * nb * 4);
+  // batches whose records the host has moved to the caller: [0, drained)
+  std::vector<std::pair<int, int>> ranges;  // pairs [n0, n1) of each batch
+  int drained = 0;
+  auto drain = [&](int upto) -> me_status {  // batches <= upto
+    for (; drained <= upto && drained < (int)ranges.size(); drained++) {
+      HIPCHK(c, hipEventSynchronize(d.d2h_ev[drained % kEvRing]));
+      const size_t o = (size_t)(ranges[drained].first - p0) * nb;
+      const size_t k = (size_t)(ranges[drained].second - ranges[drained].first) * nb;
+      memcpy(j.mv_xy + 2 * nb * p0 + 2 * o, bnc_mv + 2 * o, k * 4);
+      if (j.block_cost) memcpy(j.block_cost + nb * p0 + o, bnc_cost + o, k * 4);
+    }
+    return ME_OK;
+  };
 
   std::vector<int> last_use(j.n_frames, -1), slot_of(j.n_frames, -1);
   for (int n = p0; n < p1; n++) {
@@ -207,9 +242,12 @@ me_status run_pairs(me_ctx* c, Dev& d, const Job& j, int p0, int p1) {
   std::vector<SearchJob> jobs;
   jobs.reserve((size_t)G);
   int batch = 0;
-  // Batches ramp up 1, 2, 4, ... G pairs: the first search starts after two
-  // uploads instead of G + 1, and the next batch's uploads overlap it.
-  for (int n0 = p0, gb = 1; n0 < p1; n0 += gb, gb = std::min(2 * gb, G), batch++) {
+  // Batches ramp up 1, 2, 3, 4, 6, then G pairs: the first search starts after
+  // two uploads instead of G + 1.  A batch's new frames upload while the batch
+  // before it searches, and one upload (42 us at 1080p) is 0.6-0.7 of a pair's
+  // search, so batches may grow by about 1.5x: doubling left the GPU idle
+  // 27, 55 and 128 us before the 2-, 4- and 8-pair searches (profiles/r04m_*).
+  for (int n0 = p0, gb = 1; n0 < p1; n0 += gb, gb = std::min(gb + std::max(1, gb / 2), G), batch++) {
     if (tuning().stream_batch > 0) gb = G;  // tuning build: fixed batches (the round-3 behaviour)
     const int n1 = std::min(p1, n0 + gb);
     if (kAhead <= 8 && batch >= kAhead) {
@@ -273,6 +311,19 @@ me_status run_pairs(me_ctx* c, Dev& d, const Job& j, int p0, int p1) {
     if ((s = me::attach_scratch(c, d, base, false, n1 - n0)) != ME_OK) return s;
     if ((s = me::launch_jobs_ordered(c, d, base, jobs.data(), n1 - n0, d.stream)) != ME_OK) return s;
     HIPCHK(c, hipEventRecord(d.batch_ev[batch % kEvRing], d.stream));
+    {
+      // this batch's records: downloaded after its search, beside the next ones
+      const size_t o = (size_t)(n0 - p0) * nb, k = (size_t)(n1 - n0) * nb;
+      HIPCHK(c, hipStreamWaitEvent(d.d2h, d.batch_ev[batch % kEvRing], 0));
+      HIPCHK(c, hipMemcpyAsync(bnc_mv + 2 * o, out_mv + 2 * o, k * 4, hipMemcpyDeviceToHost, d.d2h));
+      if (j.block_cost)
+        HIPCHK(c, hipMemcpyAsync(bnc_cost + o, out_cost + o, k * 4, hipMemcpyDeviceToHost, d.d2h));
+      HIPCHK(c, hipEventRecord(d.d2h_ev[batch % kEvRing], d.d2h));
+      ranges.emplace_back(n0, n1);
+    }
+    // Move the records of batches the host already waited for (their downloads
+    // are done or nearly), and never let the event ring wrap.
+    if ((s = drain(std::max(synced - 1, batch - kEvRing + 2))) != ME_OK) return s;
     for (int n = n0; n < n1; n++)
       for (int side = 0; side < 2; side++) {
         const int f = j.pairs[2 * n + side];
@@ -284,11 +335,7 @@ me_status run_pairs(me_ctx* c, Dev& d, const Job& j, int p0, int p1) {
         }
       }
   }
-  HIPCHK(c, hipMemcpyAsync(j.mv_xy + 2 * nb * p0, out_mv, np * nb * 4, hipMemcpyDeviceToHost,
-                           d.stream));
-  if (j.block_cost)
-    HIPCHK(c, hipMemcpyAsync(j.block_cost + nb * p0, out_cost, np * nb * 4,
-                             hipMemcpyDeviceToHost, d.stream));
+  if ((s = drain(batch)) != ME_OK) return s;
   return me::device_status(c, d, d.stream);
 }
 

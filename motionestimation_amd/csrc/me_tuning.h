@@ -32,7 +32,7 @@ struct Tuning {
                           // the workgroup (-1 = automatic: the kernel path, ME_PATH_MFMA_LEAN)
   int mfma_s2r = 0;       // ME_MFMA_S2R=1|2: lean path block rows per workgroup (0 = automatic: 2 from S = 48)
   int mfma_batch = -1;    // ME_MFMA_BATCH=0|1: equal SSD jobs share matrix-core launches (-1 = automatic: on)
-  int item_batch = -1;    // ME_ITEM_BATCH=0|1: item-kernel jobs share launches (-1 = by size)
+  int item_batch = -1;    // ME_ITEM_BATCH=0: item-kernel jobs launch one by one (diagnostic)
   int ahead = -1;         // ME_AHEAD=1|2: item-kernel tiles claimed ahead (-1 = automatic)
   int strip = -1;         // ME_STRIP=0..64: item-kernel tile strips (0 = row-major; -1 = automatic)
 };

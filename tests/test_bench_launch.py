@@ -65,15 +65,13 @@ def test_exact_absdiff_count():
 
 def test_frames_per_launch_pricing():
     """bench.py prices the roofline per launch with the library's batching rules:
-    SAD batches share one launch of up to MAX_JOBS frames except frames of
-    >= 2^33 window positions (8K 8x8 +-128), which launch one by one
-    (me_kernels.hip launch_item_jobs); 8x8 SSD launches per frame."""
+    SAD batches share one launch of up to MAX_JOBS frames, 8K 8x8 +-128
+    included (me_kernels.hip launch_item_jobs); 8x8 SSD launches per frame."""
     sys.path.insert(0, REPO)
     import bench
     assert bench.sad_frames_per_launch(1920, 1080, 16, 32, 16) == 16
     assert bench.sad_frames_per_launch(3840, 2160, 16, 64, 16) == 16
     assert bench.sad_frames_per_launch(3840, 2160, 16, 64, 64) == bench.MAX_JOBS
-    assert bench.sad_frames_per_launch(7680, 4320, 8, 128, 16) == 1
-    # an 8-way stripe of the 8K frame (68 block rows) still batches
+    assert bench.sad_frames_per_launch(7680, 4320, 8, 128, 16) == 16
     assert bench.sad_frames_per_launch(7680, 68 * 8, 8, 128, 16) == 16
     assert bench.ssd_frames_per_launch(7680, 4320, 8, 128, 16) == 1
