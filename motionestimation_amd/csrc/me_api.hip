@@ -63,6 +63,8 @@ static Tuning read_tuning() {
   env_int("ME_STREAM_COOL", 1, 64, &t.stream_cool);
   env_int("ME_STREAM_AHEAD", 1, 9, &t.stream_ahead);
   env_int("ME_STREAM_BATCH", 1, 32, &t.stream_batch);
+  env_int("ME_STREAM_RAMP", 0, 1, &t.stream_ramp);
+  env_int("ME_STREAM_D2H", 0, 1, &t.stream_d2h);
   env_int("ME_FLOW", 0, 1, &t.flow);
   env_int("ME_FLOW_SLOTS", 2, 16, &t.flow_slots);
   env_int("ME_PRIO", 0, 1, &t.prio);

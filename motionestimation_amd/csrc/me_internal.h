@@ -61,10 +61,11 @@ struct Dev {
   hipEvent_t batch_ev[16] = {};
   uint8_t* pair_out = nullptr;  // [pairs][nblocks] mv records, then [pairs][nblocks] costs
   size_t pair_out_cap = 0;
-  // Records leave per batch, overlapped with the later batches' searches: a
-  // download stream waits for the batch's search and copies its records into
-  // pinned `bounce` (pair_out's layout); the host moves them to the caller's
-  // arrays while it would otherwise wait for the GPU.
+  // Records leave per batch, overlapped with the later batches' searches: the
+  // copy stream (or, tuning build, a stream of their own) waits for the
+  // batch's search and copies its records into pinned `bounce` (pair_out's
+  // layout); the host moves them to the caller's arrays while it would
+  // otherwise wait for the GPU.
   hipStream_t d2h = nullptr;
   hipEvent_t d2h_ev[16] = {};
   uint8_t* bounce = nullptr;

@@ -46,6 +46,20 @@ struct SearchArgs {
   size_t merge_tiles;
 };
 
+// Write block `out`'s MV from a merged 64-bit key (cost << 32 | (dy + 32768)
+// << 16 | (dx + 32768)): one 4-byte store of the (mvx, mvy) int16 pair when the
+// records are 4-byte aligned, else two 2-byte stores.  (8K 8x8 WRITE_SIZE reads
+// 2x the record bytes either way: a tile's 8 blocks store 32 contiguous bytes
+// per array, below the 64-byte write granule the counter appears to tally.)
+__device__ __forceinline__ void store_mv(int16_t* mv, int out, unsigned long long kk) {
+  if (((uintptr_t)mv & 3) == 0) {
+    reinterpret_cast<uint32_t*>(mv)[out] = (uint32_t)kk ^ 0x80008000u;
+  } else {
+    mv[2 * out] = (int16_t)((int)(kk & 0xFFFF) - 32768);
+    mv[2 * out + 1] = (int16_t)((int)((kk >> 16) & 0xFFFF) - 32768);
+  }
+}
+
 struct QsadGeom {
   int tb;          // blocks per workgroup
   int rows_alloc;  // LDS tile rows (chunks*K + B - 1)

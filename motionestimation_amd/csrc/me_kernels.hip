@@ -843,8 +843,7 @@ __global__ __launch_bounds__(1024) void me_fast_kernel(SearchArgs p, QsadGeom g,
         keys[tid] = none;  // ready for this workgroup's next tile
         const int out = (it.by - jb.r0[it.j]) * p.nbx + it.bx0 + tid;
         int16_t* mv = jb.mv[it.j];
-        mv[2 * out] = (int16_t)((int)(kk & 0xFFFF) - 32768);
-        mv[2 * out + 1] = (int16_t)((int)((kk >> 16) & 0xFFFF) - 32768);
+        store_mv(mv, out, kk);
         uint32_t cost = (uint32_t)(kk >> 32);
         if constexpr (COST == COST_SSD) {  // biased v -> SSD: + sum c^2 of the block
           const uint32_t* cb = reinterpret_cast<const uint32_t*>(buf + g.tile_bytes) + tid * B * CW;
@@ -1195,8 +1194,7 @@ __global__ __launch_bounds__(1024) void me_flow_kernel(SearchArgs p, QsadGeom g,
         keys[slot * g.tb + lane] = ~0ull;
         const int out = (it.by - jb.r0[it.j]) * p.nbx + it.bx0 + lane;
         int16_t* mv = jb.mv[it.j];
-        mv[2 * out] = (int16_t)((int)(kk & 0xFFFF) - 32768);
-        mv[2 * out + 1] = (int16_t)((int)((kk >> 16) & 0xFFFF) - 32768);
+        store_mv(mv, out, kk);
         if (jb.cost[it.j]) jb.cost[it.j][out] = (uint32_t)(kk >> 32);
       }
       if (lane == 0) __hip_atomic_store(&ctl->done[slot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);

@@ -632,8 +632,7 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd16_kernel(SearchArgs p, 
         nwt == 1 ? keys[tid]
                  : __hip_atomic_exchange(gk, ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int out = (br0 + br - p.block_row_begin) * p.nbx + bc0 + bc;
-    p.mv[2 * out] = (int16_t)((int)(kk & 0xFFFF) - 32768);
-    p.mv[2 * out + 1] = (int16_t)((int)((kk >> 16) & 0xFFFF) - 32768);
+    store_mv(p.mv, out, kk);
     if (p.cost) p.cost[out] = (uint32_t)(kk >> 32);
   }
   if (last && nwt > 1 && tid == 0)
@@ -891,8 +890,7 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd8_kernel(SearchArgs p, M
   if (tid < 16 && br < nbr && bc < nbc) {
     const unsigned long long kk = keys[tid];
     const int out = (br0 + br - p.block_row_begin) * p.nbx + bc0 + bc;
-    p.mv[2 * out] = (int16_t)((int)(kk & 0xFFFF) - 32768);
-    p.mv[2 * out + 1] = (int16_t)((int)((kk >> 16) & 0xFFFF) - 32768);
+    store_mv(p.mv, out, kk);
     if (p.cost) p.cost[out] = (uint32_t)(kk >> 32);
   }
 }
@@ -1246,8 +1244,7 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_bm16_kernel(SearchArgs p, M
   if (tid < nb) {
     const unsigned long long kk = keys[tid];
     const int out = (br - p.block_row_begin) * p.nbx + bc0 + tid;
-    p.mv[2 * out] = (int16_t)((int)(kk & 0xFFFF) - 32768);
-    p.mv[2 * out + 1] = (int16_t)((int)((kk >> 16) & 0xFFFF) - 32768);
+    store_mv(p.mv, out, kk);
     if (p.cost) p.cost[out] = (uint32_t)(kk >> 32);
   }
 }
@@ -1698,8 +1695,7 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_bmv_kernel(SearchArgs p, Mf
     if (r < nrw && j < nb) {
       const unsigned long long kk = keys[tid];
       const int out = (br0 + r - p.block_row_begin) * p.nbx + bc0 + j;
-      p.mv[2 * out] = (int16_t)((int)(kk & 0xFFFF) - 32768);
-      p.mv[2 * out + 1] = (int16_t)((int)((kk >> 16) & 0xFFFF) - 32768);
+      store_mv(p.mv, out, kk);
       if (p.cost) p.cost[out] = (uint32_t)(kk >> 32);
     }
   }

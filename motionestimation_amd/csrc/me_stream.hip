@@ -19,9 +19,9 @@
 //     launches delayed each launch by 58-74 us (profiles/r04e_*);
 //   - frames in me_host_alloc memory are DMAed directly, other frames are
 //     staged through two pinned buffers;
-//   - each batch's MV records are downloaded (pinned bounce buffer, own stream)
-//     after its search and moved to the caller's arrays while later batches
-//     search: one copy at the end took 250 us of host time at 64 1080p pairs.
+//   - each batch's MV records are downloaded (pinned bounce buffer, copy
+//     stream) after its search and moved to the caller's arrays while later
+//     batches search: one copy at the end took 250 us at 64 1080p pairs.
 // With several context devices the pair list is cut into contiguous runs,
 // one per device, each driven by its own host thread (independent pairs: no
 // collective).
@@ -110,13 +110,13 @@ me_status prepare(me_ctx* c, Dev& d, size_t plane) {
     d.slot_bytes = plane;
   }
   if (!d.copy) HIPCHK(c, hipStreamCreateWithFlags(&d.copy, hipStreamNonBlocking));
-  if (!d.d2h) HIPCHK(c, hipStreamCreateWithFlags(&d.d2h, hipStreamNonBlocking));
+  if (!d.d2h && tuning().stream_d2h == 1) HIPCHK(c, hipStreamCreateWithFlags(&d.d2h, hipStreamNonBlocking));
   for (int k = 0; k < kEvRing; k++) {
     if (!d.upl_ev[k]) HIPCHK(c, hipEventCreateWithFlags(&d.upl_ev[k], hipEventDisableTiming));
     if (!d.batch_ev[k]) HIPCHK(c, hipEventCreateWithFlags(&d.batch_ev[k], hipEventDisableTiming));
     if (!d.d2h_ev[k]) HIPCHK(c, hipEventCreateWithFlags(&d.d2h_ev[k], hipEventDisableTiming));
   }
-  HIPCHK(c, hipStreamSynchronize(d.d2h));  // a failed earlier call may have left copies
+  if (d.d2h) HIPCHK(c, hipStreamSynchronize(d.d2h));  // a failed earlier call may have left copies
   return ME_OK;
 }
 
@@ -183,11 +183,33 @@ me_status run_pairs(me_ctx* c, Dev& d, const Job& j, int p0, int p1) {
   }
   int16_t* bnc_mv = reinterpret_cast<int16_t*>(d.bounce);
   uint32_t* bnc_cost = reinterpret_cast<uint32_t*>(d.bounce + np * nb * 4);
-  // batches whose records the host has moved to the caller: [0, drained)
+  // Records of batch b leave on the copy stream, queued behind batch b + 1's
+  // uploads (which must overlap batch b's search) and ahead of batch b + 2's
+  // (which the host enqueues only after batch b is done anyway).  A stream of
+  // their own measured the same alone, but one more stream than the process's
+  // hardware queues (GPU_MAX_HW_QUEUES = 4: torch's, the caller's, compute,
+  // copy) shares a queue with the search or the uploads: 13.0k instead of
+  // 14.2k pinned 1080p pairs/s after searches on a torch stream
+  // (profiles/r04r_*).  The tuning build's ME_STREAM_D2H=1 restores it.
+  const bool own_dl = d.d2h != nullptr;
+  hipStream_t dl = own_dl ? d.d2h : d.copy;
   std::vector<std::pair<int, int>> ranges;  // pairs [n0, n1) of each batch
+  int downloaded = 0;  // batches whose record copies are enqueued: [0, downloaded)
+  auto download = [&]() -> me_status {
+    const int b = downloaded++;
+    const size_t o = (size_t)(ranges[b].first - p0) * nb;
+    const size_t k = (size_t)(ranges[b].second - ranges[b].first) * nb;
+    HIPCHK(c, hipStreamWaitEvent(dl, d.batch_ev[b % kEvRing], 0));
+    HIPCHK(c, hipMemcpyAsync(bnc_mv + 2 * o, out_mv + 2 * o, k * 4, hipMemcpyDeviceToHost, dl));
+    if (j.block_cost)
+      HIPCHK(c, hipMemcpyAsync(bnc_cost + o, out_cost + o, k * 4, hipMemcpyDeviceToHost, dl));
+    HIPCHK(c, hipEventRecord(d.d2h_ev[b % kEvRing], dl));
+    return ME_OK;
+  };
+  // batches whose records the host has moved to the caller: [0, drained)
   int drained = 0;
   auto drain = [&](int upto) -> me_status {  // batches <= upto
-    for (; drained <= upto && drained < (int)ranges.size(); drained++) {
+    for (; drained <= upto && drained < downloaded; drained++) {
       HIPCHK(c, hipEventSynchronize(d.d2h_ev[drained % kEvRing]));
       const size_t o = (size_t)(ranges[drained].first - p0) * nb;
       const size_t k = (size_t)(ranges[drained].second - ranges[drained].first) * nb;
@@ -248,7 +270,7 @@ me_status run_pairs(me_ctx* c, Dev& d, const Job& j, int p0, int p1) {
   // search, so batches may grow by about 1.5x: doubling left the GPU idle
   // 27, 55 and 128 us before the 2-, 4- and 8-pair searches (profiles/r04m_*).
   for (int n0 = p0, gb = 1; n0 < p1; n0 += gb, gb = std::min(gb + std::max(1, gb / 2), G), batch++) {
-    if (tuning().stream_batch > 0) gb = G;  // tuning build: fixed batches (the round-3 behaviour)
+    if (tuning().stream_ramp == 0) gb = G;  // tuning build: fixed batches (the round-3 behaviour)
     const int n1 = std::min(p1, n0 + gb);
     if (kAhead <= 8 && batch >= kAhead) {
       HIPCHK(c, hipEventSynchronize(d.batch_ev[(batch - kAhead) % kEvRing]));
@@ -308,19 +330,13 @@ me_status run_pairs(me_ctx* c, Dev& d, const Job& j, int p0, int p1) {
       HIPCHK(c, hipEventRecord(d.upl_ev[batch % kEvRing], d.copy));
       HIPCHK(c, hipStreamWaitEvent(d.stream, d.upl_ev[batch % kEvRing], 0));
     }
+    while (!own_dl && downloaded < batch)  // the previous batch's records, behind these uploads
+      if ((s = download()) != ME_OK) return s;
     if ((s = me::attach_scratch(c, d, base, false, n1 - n0)) != ME_OK) return s;
     if ((s = me::launch_jobs_ordered(c, d, base, jobs.data(), n1 - n0, d.stream)) != ME_OK) return s;
     HIPCHK(c, hipEventRecord(d.batch_ev[batch % kEvRing], d.stream));
-    {
-      // this batch's records: downloaded after its search, beside the next ones
-      const size_t o = (size_t)(n0 - p0) * nb, k = (size_t)(n1 - n0) * nb;
-      HIPCHK(c, hipStreamWaitEvent(d.d2h, d.batch_ev[batch % kEvRing], 0));
-      HIPCHK(c, hipMemcpyAsync(bnc_mv + 2 * o, out_mv + 2 * o, k * 4, hipMemcpyDeviceToHost, d.d2h));
-      if (j.block_cost)
-        HIPCHK(c, hipMemcpyAsync(bnc_cost + o, out_cost + o, k * 4, hipMemcpyDeviceToHost, d.d2h));
-      HIPCHK(c, hipEventRecord(d.d2h_ev[batch % kEvRing], d.d2h));
-      ranges.emplace_back(n0, n1);
-    }
+    ranges.emplace_back(n0, n1);
+    if (own_dl && (s = download()) != ME_OK) return s;
     // Move the records of batches the host already waited for (their downloads
     // are done or nearly), and never let the event ring wrap.
     if ((s = drain(std::max(synced - 1, batch - kEvRing + 2))) != ME_OK) return s;
@@ -335,6 +351,8 @@ me_status run_pairs(me_ctx* c, Dev& d, const Job& j, int p0, int p1) {
         }
       }
   }
+  while (downloaded < batch)
+    if ((s = download()) != ME_OK) return s;
   if ((s = drain(batch)) != ME_OK) return s;
   return me::device_status(c, d, d.stream);
 }

@@ -20,7 +20,9 @@ struct Tuning {
   int mfma_ngxw = 0;      // ME_MFMA_NGXW=1|2: column groups per workgroup (0 = automatic)
   int stream_cool = 0;    // ME_STREAM_COOL=1..64: cooling frame slots (0 = automatic)
   int stream_ahead = 0;   // ME_STREAM_AHEAD=1..9: host run-ahead (9: unbounded; 0 = automatic)
-  int stream_batch = 0;   // ME_STREAM_BATCH=1..32: pairs per search launch (0 = automatic)
+  int stream_batch = 0;   // ME_STREAM_BATCH=1..32: pairs per search launch after the ramp (0 = automatic)
+  int stream_d2h = 0;     // ME_STREAM_D2H=1: pair records download on a stream of their own
+  int stream_ramp = -1;   // ME_STREAM_RAMP=0: no ramp, every launch ME_STREAM_BATCH pairs (-1 = ramp)
   int flow = -1;          // ME_FLOW=0|1: SAD flow kernel off / allowed (-1 = automatic)
   int flow_slots = 0;     // ME_FLOW_SLOTS=2..16: flow kernel LDS ring slots (0 = automatic)
   int prio = -1;          // ME_PRIO=0|1: staging waves raise their issue priority (-1 = automatic: on)
