@@ -75,6 +75,9 @@ struct QsadGeom {
   int threads;     // workgroup size
   int lds;         // dynamic LDS bytes
   int wg_per_row;  // workgroups per block row
+  uint32_t magic_wpr;  // umulhi(t, magic_wpr) == t / wg_per_row for every tile index of
+                       // the planned rows (host-checked; 0: divide)
+  uint32_t magic_tb;   // 0xFFFFFFFF / tb + 1: an item's / nb magic when nb == tb
   int strip_w;     // > 0: tiles run in vertical strips of strip_w tile columns, each
                    // strip top to bottom (wide frames: an XCD's L2 keeps the strip's
                    // window rows while the tile rows that read them pass)

@@ -522,8 +522,11 @@ __device__ __forceinline__ Item item_of(const SearchArgs& p, const QsadGeom& g, 
     it.bx0 = (s * sw + (r - row * w)) * g.tb;
     it.by = g.row0 + row;
   } else {
-    it.bx0 = (tile % g.wg_per_row) * g.tb;
-    it.by = g.row0 + tile / g.wg_per_row;
+    // row-major; the division by a multiply-high (scalar) where the host
+    // verified the magic: a VALU integer division here ran twice per item
+    const int row = g.magic_wpr ? (int)__umulhi((uint32_t)tile, g.magic_wpr) : tile / g.wg_per_row;
+    it.bx0 = (tile - row * g.wg_per_row) * g.tb;
+    it.by = g.row0 + row;
   }
   it.nb = min(g.tb, g.nbx_full - it.bx0);
   it.tly = it.by * B;
@@ -702,6 +705,7 @@ __global__ __launch_bounds__(1024) void me_fast_kernel(SearchArgs p, QsadGeom g,
   __syncthreads();
 
   int ti = 0, pass = 0;
+  int rot = bid % (nthr >> 6);
 #ifdef ME_STAMPS
   int nitems = 0;
 #endif
@@ -744,12 +748,13 @@ __global__ __launch_bounds__(1024) void me_fast_kernel(SearchArgs p, QsadGeom g,
     const int T = (lc1 - lc0) * per_chunk;
     // task t -> (chunk, block, group) by multiply-high: t / G with the host's
     // verified magic, then / nb with a per-item magic (nb <= 16).
-    const uint32_t magic_nb = 0xFFFFFFFFu / (uint32_t)it.nb + 1u;
+    const uint32_t magic_nb = it.nb == g.tb ? g.magic_tb : 0xFFFFFFFFu / (uint32_t)it.nb + 1u;
     // When T is not a multiple of the workgroup size the last round falls to
     // the first waves; rotate which wave that is from item to item so no SIMD
-    // takes every extra round.
-    int vt = fresh_tid() - 64 * ((bid + k) % (nthr >> 6));
+    // takes every extra round (rot == (bid + k) % waves, kept as a counter).
+    int vt = fresh_tid() - 64 * rot;
     if (vt < 0) vt += nthr;
+    rot = rot + 1 == (nthr >> 6) ? 0 : rot + 1;
     for (int t = vt; t < T; t += nthr) {
       const int bg = (int)__umulhi((uint32_t)t, g.magic_groups);  // t / G
       const int gi = t - bg * G;
@@ -809,7 +814,18 @@ __global__ __launch_bounds__(1024) void me_fast_kernel(SearchArgs p, QsadGeom g,
       const int dxg = 4 * gi - S - it.a;  // dx of this lane's first candidate
       const bool edge = dxg < dxmin || dxg + 3 > dxmax;
       uint32_t best;
-      if (full_rows && __builtin_amdgcn_ballot_w64(edge) == 0) {
+      const bool no_edge = __builtin_amdgcn_ballot_w64(edge) == 0;
+      const int sjlo = __builtin_amdgcn_readfirstlane(jlo), sjhi = __builtin_amdgcn_readfirstlane(jhi);
+      if (no_edge && (full_rows || __builtin_amdgcn_ballot_w64(jlo != sjlo || jhi != sjhi) == 0)) {
+        // Rows partial only (the last dy chunk, the top and bottom block rows)
+        // with one row range for the wave: park the invalid rows at SAD 0xFFFF
+        // (scalar tests, a move only where a row is out) and take the unmasked
+        // epilogue; the masked one tests every row of every lane.
+        if (!full_rows) {
+#pragma unroll
+          for (int j = 0; j < K; j++)
+            if (j < sjlo || j > sjhi) acc[j] = ~0ull;
+        }
         best = lane_best<K, false>(acc, 0u, 0u, jlo, jhi);
       } else {
         uint32_t mlo = 0, mhi = 0;
@@ -1431,6 +1447,18 @@ bool plan_fast(const SearchArgs& p, QsadGeom* g, int* k_out) {
   for (uint32_t d = 0; d < (uint32_t)g->tile_bytes; d += 4)
     if ((uint32_t)(((uint64_t)d * g->pitch_magic) >> 32) != d / (uint32_t)g->pitch) return false;
   g->wg_per_row = (g->nbx_full + g->tb - 1) / g->tb;
+  {
+    // t / wg_per_row by multiply-high for every tile index of these rows
+    const uint32_t d = (uint32_t)g->wg_per_row, m = 0xFFFFFFFFu / d + 1u;
+    const uint32_t nt = (uint32_t)g->wg_per_row * (uint32_t)(rows > 0 ? rows : 1);
+    g->magic_wpr = m;
+    for (uint32_t t = 0; t < nt; t++)
+      if ((uint32_t)(((uint64_t)t * m) >> 32) != t / d) {
+        g->magic_wpr = 0;
+        break;
+      }
+    g->magic_tb = 0xFFFFFFFFu / (uint32_t)g->tb + 1u;
+  }
   g->aligned = (p.stride % 4 == 0) && ((uintptr_t)p.ref % 4 == 0) && ((uintptr_t)p.cur % 4 == 0);
   // X0 = tb*B*t - S - a is 16-aligned for every tile when a = 0 (S % 4 == 0),
   // S % 16 == 0 and tb * B % 16 == 0; rows of the ref plane 16-aligned; W % 16
@@ -1554,6 +1582,8 @@ bool plan_flow(const SearchArgs& p, QsadGeom* g) {
   q.rows_alloc = chunks * K + B - 1;
   q.tile_bytes = q.rows_alloc * q.pitch;
   q.wg_per_row = (nbx_full + q.tb - 1) / q.tb;
+  q.magic_wpr = 0;  // the flow kernel maps a tile once per item: plain division
+  q.magic_tb = 0xFFFFFFFFu / (uint32_t)q.tb + 1u;
   q.aligned = 1;
   q.tile16 = 1;
   q.threads = 1024;

@@ -26,7 +26,12 @@ for d in sorted(glob.glob(os.path.join(out, "v*/")), key=lambda p: int(p.rstrip(
     top = max(v["dur"] for v in ds)
     big = [v for v in ds if v["dur"] >= 0.5 * top]
     mean = lambda key: sum(v.get(key, 0) for v in big) / len(big)
-    rd = 128 * mean("TCC_EA0_RDREQ_128B_sum") + 64 * mean("TCC_EA0_RDREQ_64B_sum")
-    h, m = mean("TCC_HIT_sum"), mean("TCC_MISS_sum")
-    print(f"{name:40s} {kern[-40:]:40s} n {len(big):3d}  {mean('dur') / 1e3:9.1f} us  "
-          f"read {rd / 1e6:8.1f} MB  L2 hit {h / max(h + m, 1):.4f}")
+    if "TCC_EA0_RDREQ_128B_sum" in big[0]:
+        rd = 128 * mean("TCC_EA0_RDREQ_128B_sum") + 64 * mean("TCC_EA0_RDREQ_64B_sum")
+        h, m = mean("TCC_HIT_sum"), mean("TCC_MISS_sum")
+        print(f"{name:40s} {kern[-40:]:40s} n {len(big):3d}  {mean('dur') / 1e3:9.1f} us  "
+              f"read {rd / 1e6:8.1f} MB  L2 hit {h / max(h + m, 1):.4f}")
+    else:  # any other counter set: every counter's batch-launch mean
+        cs = sorted(k for k in big[0] if k != "dur")
+        print(f"{name:40s} {kern[-40:]:40s} n {len(big):3d}  {mean('dur') / 1e3:9.1f} us  " +
+              "  ".join(f"{c} {mean(c):.4g}" for c in cs))
