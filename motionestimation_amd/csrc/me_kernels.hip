@@ -814,18 +814,21 @@ __global__ __launch_bounds__(1024) void me_fast_kernel(SearchArgs p, QsadGeom g,
       const int dxg = 4 * gi - S - it.a;  // dx of this lane's first candidate
       const bool edge = dxg < dxmin || dxg + 3 > dxmax;
       uint32_t best;
-      const bool no_edge = __builtin_amdgcn_ballot_w64(edge) == 0;
-      const int sjlo = __builtin_amdgcn_readfirstlane(jlo), sjhi = __builtin_amdgcn_readfirstlane(jhi);
-      if (no_edge && (full_rows || __builtin_amdgcn_ballot_w64(jlo != sjlo || jhi != sjhi) == 0)) {
-        // Rows partial only (the last dy chunk, the top and bottom block rows)
-        // with one row range for the wave: park the invalid rows at SAD 0xFFFF
+      bool unmasked = __builtin_amdgcn_ballot_w64(edge) == 0;
+      if (unmasked && !full_rows) {
+        // Rows partial only (the last dy chunk, the top and bottom block rows):
+        // with one row range for the wave, park the invalid rows at SAD 0xFFFF
         // (scalar tests, a move only where a row is out) and take the unmasked
         // epilogue; the masked one tests every row of every lane.
-        if (!full_rows) {
+        const int sjlo = __builtin_amdgcn_readfirstlane(jlo), sjhi = __builtin_amdgcn_readfirstlane(jhi);
+        unmasked = __builtin_amdgcn_ballot_w64(jlo != sjlo || jhi != sjhi) == 0;
+        if (unmasked) {
 #pragma unroll
           for (int j = 0; j < K; j++)
             if (j < sjlo || j > sjhi) acc[j] = ~0ull;
         }
+      }
+      if (unmasked) {
         best = lane_best<K, false>(acc, 0u, 0u, jlo, jhi);
       } else {
         uint32_t mlo = 0, mhi = 0;
