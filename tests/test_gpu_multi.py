@@ -105,8 +105,9 @@ def test_library_communicator_one_rank():
 def test_comm_check_one_rank():
     """me_comm_check (failure detection of the exchange): clean after a
     gather on a one-rank group; when the stream's work outlasts the timeout it
-    returns ME_ECOMM and aborts the communicator, the stream still drains, and
-    every later gather or check fails loudly instead of hanging."""
+    returns ME_ECOMM and aborts the communicator, the stream still drains,
+    every later gather or check fails loudly instead of hanging, and a new
+    me_comm_init recovers the context."""
     import torch
     with me.Engine(devices=[0]) as eng:
         with pytest.raises(me.MEError):  # no communicator yet
@@ -139,6 +140,13 @@ def test_comm_check_one_rank():
             eng.comm_check(1000)
         assert e.value.status == me.ME_ECOMM
         eng.device_check()
+        # a new communicator (fresh id, every rank) makes the context usable again
+        eng.comm_init(eng.comm_unique_id(), 1, 0)
+        dst.zero_()
+        src1 = src + 1
+        eng.gather_device(src1, dst)
+        eng.comm_check(10_000)
+        assert torch.equal(dst[0], src1)
 
 
 def _bench_ranks(nproc, backend, extra=()):
