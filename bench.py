@@ -69,6 +69,8 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-ssd", action="store_true",
                     help="skip the SSD (matrix-core) line beside a SAD run")
+    ap.add_argument("--no-ssim", action="store_true",
+                    help="skip the SSIM-cost leg beside a 1080p SAD run")
     ap.add_argument("--no-stream", action="store_true",
                     help="skip the host frame-pair streaming leg (PCIe-inclusive, not `value`)")
     ap.add_argument("--cpu-threads", type=int, default=None,
@@ -86,7 +88,12 @@ def parse():
                     help="frames searched per step: one batched launch per rank "
                          "(me_full_search_batch_device) and, in stripe mode, one gather per step")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
-                    help="nccl = RCCL (production); gloo only to rehearse N ranks on one GPU")
+                    help="the data exchange: nccl = the library's RCCL gather (production); gloo "
+                         "= torch.distributed.gather, only to rehearse N ranks on one GPU.  "
+                         "torch's own process group (control plane) is gloo either way")
+    ap.add_argument("--torch-pg", choices=["gloo", "nccl"], default="gloo",
+                    help="torch.distributed's own process group (control plane); nccl only to "
+                         "A/B the round-4 configuration (a second RCCL communicator per rank)")
     ap.add_argument("--comm-timeout-ms", type=int, default=60000,
                     help="RCCL ranks: bounded wait for a step's searches + gather (me_comm_check); "
                          "past it the rank aborts its communicator and exits non-zero")
@@ -254,6 +261,7 @@ def host_stream(eng, w, h, blk, span, cost, seed, sx, sy, frame_ms, batch_frame_
     pageable = np.array(pinned)
     pairs = [(k, k + 1) for k in range(npairs)]
     out = {"pairs": npairs, "workload": f"{npairs + 1}-frame pan, consecutive pairs"}
+    last = {}
     for name, frames in (("pinned", list(pinned)), ("pageable", list(pageable))):
         eng.search_pairs(frames, pairs, blk, span, cost)  # allocates the device slots
         t0 = time.perf_counter()  # clock ramp, as before the other legs (warm())
@@ -262,10 +270,23 @@ def host_stream(eng, w, h, blk, span, cost, seed, sx, sy, frame_ms, batch_frame_
         reps = 3
         t0 = time.perf_counter()
         for _ in range(reps):
-            eng.search_pairs(frames, pairs, blk, span, cost)
+            res = eng.search_pairs(frames, pairs, blk, span, cost)
         dt = (time.perf_counter() - t0) / reps
+        last[name] = res
         out[name] = {"pairs_per_s": npairs / dt, "candidates_per_s": cands_frame * npairs / dt,
                      "ms_per_pair": dt / npairs * 1e3}
+    # The last timed call's records (both memories) against each pair searched
+    # on its own (me_full_search: another entry point, one frame per launch).
+    bad = []
+    for k, (r, q) in enumerate(pairs):
+        smv, sco = eng.full_search(pageable[r], pageable[q], blk, span, cost)
+        for name in ("pinned", "pageable"):
+            mv, co = last[name]
+            if not (np.array_equal(mv[k], smv) and np.array_equal(co[k], sco)):
+                bad.append(f"{name} pair {k}")
+    out["parity"] = {"ok": not bad, "pairs_checked": npairs, "mismatches": bad[:8],
+                     "what": "the last timed call's records (pinned and pageable frames) == "
+                             "me_full_search of each pair"}
     # the kernels alone, inputs in HBM: one frame per launch, and per frame of
     # a batched launch
     out["kernel_only_pairs_per_s"] = 1e3 / frame_ms
@@ -339,6 +360,67 @@ def ssd_beside(eng, ref_t, cur_t, blk, span, nb, cands_frame, dev, steps, pins, 
             "roofline": {"bound": "mfma", "achieved": tops, "peak": I8_PEAK_TOPS,
                          "unit": "TFLOP/s", "frac": tops / I8_PEAK_TOPS},
             "parity": par}
+
+
+def ssim_beside(eng, ref_t, cur_t, blk, span, nb, dev, steps, ramp_ms):
+    """The reference's SSIM search (src/common/ssim.c:44-108, ME_COST_SSIM) on
+    frame 0 of the step (the committed golden ssim_synth1080p_b16_s32 is the
+    unmodified reference's own field of this pair), one frame per call.  The
+    search replays the reference's float chain: per candidate pixel one exact
+    fma (the cross term, rounded where the reference's `cv +=` rounds) and one
+    subtract, so the fp32 VALU issue fraction counts 2 lane-instructions per
+    candidate pixel against the vector issue peak (157.3 TFLOPS / 2 flops per
+    fma = 78.6e12 lane-instructions/s)."""
+    import torch
+    import motionestimation_amd as me
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    h, w = ref_t.shape
+    mv = torch.empty((nb, 2), dtype=torch.int16, device=dev)
+    co = torch.empty(nb, dtype=torch.int32, device=dev)
+    run = lambda: eng.full_search_device(ref_t, cur_t, blk, span, "ssim", mv, co)  # noqa: E731
+    warm(run, ramp_ms)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(steps):
+        run()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / steps
+    cands = me.candidate_count(w, h, blk, span)
+    pix = exact_absdiffs(w, h, blk, span)  # candidate pixels: sum of w*h x candidates
+    lane_ops = 2.0 * pix
+    peak_lane = 157.3e12 / 2
+    out = {"value": cands / (ms / 1e3), "unit": "candidates/s", "kernel_ms": ms, "steps": steps,
+           "workload": f"{w}x{h} Y, {blk}x{blk}, +-{span}, SSIM (reference ssim.c float order, "
+                       "bit-exact), one frame per call",
+           "roofline": {"bound": "valu_fp32", "achieved_lane_instr_per_s": lane_ops / (ms / 1e3),
+                        "peak_lane_instr_per_s": peak_lane,
+                        "frac": lane_ops / (ms / 1e3) / peak_lane,
+                        "flops_frac": 3.0 * pix / (ms / 1e3) / 157.3e12,
+                        "note": "2 fp32 lane-instructions (fma + sub) per candidate pixel, the "
+                                "kernel's exact cross chain; statistics prepass included in the time"}}
+    par = {"ok": False, "golden": None}
+    try:
+        import oracle_lib as O
+        man = O.manifest()
+        case = [c for c in man["ssim_cases"] if c["width"] == w and c["height"] == h and
+                c["blk"] == blk and c["span"] == span]
+        if case:
+            gmv, gscore = O.load_case(case[0])
+            dc = device_check(eng)
+            mvh, bits = mv.cpu().numpy(), co.cpu().numpy().view(np.uint32)
+            pos = gscore > 0
+            eq = bool(np.array_equal(bits, gscore.view(np.uint32)) and
+                      np.array_equal(mvh[pos].astype(np.int32), gmv[pos]) and
+                      not mvh[~pos].any())
+            par = {"ok": eq and dc == "ok", "device_check": dc, "golden": case[0]["name"],
+                   "pin_source": "tests/golden: unmodified reference SSIM search (ref_dump_ssim)",
+                   "score_bits_equal": bool(np.array_equal(bits, gscore.view(np.uint32)))}
+    except (OSError, ValueError, KeyError) as e:  # golden unreadable: reported, leg fails
+        par = {"ok": False, "error": str(e)}
+    out["parity"] = par
+    return out
 
 
 def batch_frames(ref, cur, nframes):
@@ -505,7 +587,8 @@ class StripeRun:
         self.graphs = None
         if self.lib:
             if not eng.comm_ranks:  # one communicator per context (stripe_4k reuses it)
-                uid = torch.zeros(128, dtype=torch.uint8, device=dev)
+                uid = torch.zeros(128, dtype=torch.uint8,  # host tensor on the gloo control plane
+                                  device=dev if dist.get_backend() == "nccl" else "cpu")
                 if rank == 0:
                     uid.copy_(torch.frombuffer(bytearray(eng.comm_unique_id()), dtype=torch.uint8))
                 dist.broadcast(uid, 0)
@@ -860,10 +943,17 @@ def main():
         # fail after this instead of the default 10 minutes
         import datetime
         tmo = datetime.timedelta(seconds=max(60, 3 * args.comm_timeout_ms // 1000))
-        if gloo:
-            dist.init_process_group("gloo", timeout=tmo)
-        else:
+        # torch's process group is the control plane only (the id broadcast,
+        # barriers, the ramp's MIN and the result's MAX, on host tensors): gloo
+        # in both modes.  The one data exchange of an RCCL run is the library's
+        # ncclGather (me_gather_device), so a rank holds ONE RCCL communicator
+        # and its streams: with torch's "nccl" group as well, a rank held two
+        # communicators on top of torch's stream and the search stream, more
+        # streams than GPU_MAX_HW_QUEUES = 4.
+        if args.torch_pg == "nccl" and not gloo:  # A/B only: the round-4 configuration
             dist.init_process_group("nccl", device_id=dev, timeout=tmo)
+        else:
+            dist.init_process_group("gloo", timeout=tmo)
 
     import motionestimation_amd as me
     from motionestimation_amd import synth
@@ -1015,6 +1105,11 @@ def main():
                                       min(args.steps, 20), load_pins(args.config, blk, span, "ssd"),
                                       args.ramp_ms)
         legs["ssd_mfma"] = line["ssd_mfma"]["parity"]
+    if (rank == 0 and world == 1 and mode == "frames" and args.config == "1080p"
+            and args.cost == "sad" and not args.no_ssim):
+        line["ssim"] = ssim_beside(eng, ref_t[0], cur_t[0], blk, span, nb, dev,
+                                   min(args.steps, 10), args.ramp_ms)
+        legs["ssim"] = line["ssim"]["parity"]
     if rank == 0 and world == 1 and not args.no_cpu:
         line["cpu_baseline"], field = cpu_baselines(ref, cur, blk, span, args.cost,
                                                     args.cpu_threads, cands_frame)
@@ -1039,6 +1134,7 @@ def main():
         one = line.get("single_frame", {}).get("kernel_ms", kern_ms / F)
         line["host_stream"] = host_stream(eng, w, h, blk, span, args.cost, seed, sx, sy,
                                           one, kern_ms / F, cands_frame, args.ramp_ms)
+        legs["host_stream"] = line["host_stream"]["parity"]
     ok = all(leg["ok"] for leg in legs.values())
     line["parity"] = ok
     line["parity_legs"] = legs

@@ -89,23 +89,29 @@ const char* me_last_error(const me_ctx* ctx);
 /* Library version string, e.g. "me_hip 1 gfx950". */
 const char* me_version(void);
 
-/* Kernel path (process-wide; A/B tests and diagnostics).  ME_PATH_AUTO: SSD
- * searches with 16x16 and 8x8 blocks run on the matrix cores (i8 MFMA),
- * everything else on the VALU kernels; ME_PATH_VALU: VALU kernels only;
- * ME_PATH_MFMA_TILES: as AUTO, but 16x16 SSD on the 4x4-block-tile MFMA kernel
- * (the fallback for rows that are not 16-byte aligned) instead of the
- * block-major one; ME_PATH_MFMA_LEAN: as AUTO, but 16x16 SSD with S <= 64
- * forms its S2 term inside the search kernel instead of reading the prepass
- * planes: no context scratch (AUTO holds 5 bytes per reference pixel of it per
- * frame of a batch) and ~1.2x the algorithmic HBM bytes instead of ~7.5x, at
- * ~1.4x the kernel time.  Results are identical on every path.
- * The environment variable ME_PATH=auto|valu|tiles|lean sets the initial value
- * (anything else is ignored with a message on stderr). */
+/* Kernel path (process-wide; A/B tests and diagnostics).  Results are
+ * identical on every path.
+ *   ME_PATH_AUTO: SSD with 16x16 and 8x8 blocks on the matrix cores (i8 MFMA),
+ *     everything else on the VALU kernels.  16x16 SSD with S <= 64 runs the
+ *     band-walk kernel: each 16-row band's S2 term formed once in LDS for
+ *     every block row in flight, no context scratch, ~1.1x the algorithmic
+ *     HBM bytes; larger ranges the prepass + block-major pair.
+ *   ME_PATH_VALU: VALU kernels only.
+ *   ME_PATH_MFMA_TILES: 16x16 SSD on the 4x4-block-tile MFMA kernel (the
+ *     fallback for rows that are not 16-byte aligned).
+ *   ME_PATH_MFMA_LEAN: 16x16 SSD with S <= 64 forms its S2 term per
+ *     workgroup and band (me_mfma_bmv_kernel, the kernel that also takes a
+ *     partial bottom block row on the AUTO path).
+ *   ME_PATH_MFMA_PREPASS: 16x16 SSD on the S2 prepass + block-major kernel
+ *     (5 bytes of context scratch per reference pixel per frame of a batch).
+ * The environment variable ME_PATH=auto|valu|tiles|lean|prepass sets the
+ * initial value (anything else is ignored with a message on stderr). */
 typedef enum {
   ME_PATH_AUTO = 0,
   ME_PATH_VALU = 1,
   ME_PATH_MFMA_TILES = 2,
-  ME_PATH_MFMA_LEAN = 3
+  ME_PATH_MFMA_LEAN = 3,
+  ME_PATH_MFMA_PREPASS = 4
 } me_path;
 void me_set_kernel_path(me_path path);
 

@@ -20,7 +20,7 @@ ME_COMM_ID_BYTES = 128  # include/me.h (sizeof ncclUniqueId)
 ME_COMM_TIMEOUT_MS = 60000
 ME_YUV_LUMA, ME_YUV_I420 = 0, 1
 ME_COST_SSD, ME_COST_SAD, ME_COST_SSIM = 0, 1, 2
-ME_PATH_AUTO, ME_PATH_VALU, ME_PATH_MFMA_TILES, ME_PATH_MFMA_LEAN = 0, 1, 2, 3
+ME_PATH_AUTO, ME_PATH_VALU, ME_PATH_MFMA_TILES, ME_PATH_MFMA_LEAN, ME_PATH_MFMA_PREPASS = 0, 1, 2, 3, 4
 ME_MAX_BLOCK, ME_MAX_RANGE = 64, 1024
 
 # Every symbol include/me.h declares, with (restype, argtypes).

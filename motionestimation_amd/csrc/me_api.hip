@@ -76,6 +76,8 @@ static Tuning read_tuning() {
   env_int("ME_MFMA_BATCH", 0, 1, &t.mfma_batch);
   env_int("ME_MFMA_S2K", 0, 1, &t.mfma_s2k);
   env_int("ME_MFMA_S2R", 1, 2, &t.mfma_s2r);
+  env_int("ME_BW", 0, 1, &t.bw);
+  env_int("ME_BW_SEG", 1, 4096, &t.bw_seg);
   if (const char* e = getenv("ME_FAIR_T")) {
     int lo = 0, hi = 0;
     if (sscanf(e, "%d,%d", &lo, &hi) == 2 && lo >= 1 && lo <= hi && hi <= 255) {
@@ -105,7 +107,8 @@ static int initial_path() {
   if (!strcmp(e, "valu")) return 1;
   if (!strcmp(e, "tiles")) return 2;
   if (!strcmp(e, "lean")) return 3;
-  fprintf(stderr, "me_hip: ignoring ME_PATH=%s (auto | valu | tiles | lean)\n", e);
+  if (!strcmp(e, "prepass")) return 4;
+  fprintf(stderr, "me_hip: ignoring ME_PATH=%s (auto | valu | tiles | lean | prepass)\n", e);
   return 0;
 }
 static std::atomic<int>& path_code() {
@@ -287,6 +290,11 @@ me_status launch_jobs_ordered(me_ctx* c, Dev& d, const SearchArgs& base, const S
   return ME_OK;
 }
 
+me_status own_stream(me_ctx* c, Dev& d) {
+  if (!d.stream) HIPCHK(c, hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+  return ME_OK;
+}
+
 me_status device_status(me_ctx* c, Dev& d, hipStream_t s) {
   uint32_t w = 0;
   HIPCHK(c, hipMemcpyAsync(&w, d.sched + SCHED_ERR, 4, hipMemcpyDeviceToHost, s));
@@ -294,8 +302,8 @@ me_status device_status(me_ctx* c, Dev& d, hipStream_t s) {
   if (w) {
     // The word is per device, so it may also hold the report of an earlier
     // asynchronous search that nobody checked yet: keep it for that caller's
-    // me_device_check as well (include/me.h).
-    d.err_pending = w;
+    // me_device_check as well (include/me.h) -- when there is such a search.
+    if (d.async_unchecked) d.err_pending = w;
     HIPCHK(c, hipMemsetAsync(d.sched + SCHED_ERR, 0, 4, s));
     HIPCHK(c, hipStreamSynchronize(s));
     return fail(c, ME_EDEVICE, "device %d: a search kernel's bounded wait expired (code %u): "
@@ -423,6 +431,8 @@ me_status stripe_upload_launch(me_ctx* c, Dev& d, const uint8_t* ref, const uint
                                int width, int height, int stride, int blk, int range, int cost,
                                int r0, int r1, size_t max_blocks) {
   HIPCHK(c, hipSetDevice(d.id));
+  me_status s0 = me::own_stream(c, d);
+  if (s0 != ME_OK) return s0;
   const int y_ref0 = r0 * blk - range > 0 ? r0 * blk - range : 0;
   const int y_ref1 = r1 * blk + range < height ? r1 * blk + range : height;
   const int y_cur0 = r0 * blk;
@@ -484,27 +494,54 @@ me_status multi_search(me_ctx* c, const uint8_t* ref, const uint8_t* cur, int wi
   if ((s = grow(c, (void**)&root.gather, &root.gather_cap, rec_bytes * n)) != ME_OK) return s;
   if (c->distinct) {
     if ((s = ensure_comms(c)) != ME_OK) return s;
-    NCCLCHK(c, ncclGroupStart());
+    // The searches end on their own (their kernels' waits are bounded): mark
+    // each one's end, so that the bounded RCCL wait below covers the gather
+    // alone, not a long search (8K 8x8 SSIM at a large range takes minutes).
+    std::vector<hipEvent_t> done(n, nullptr);
+    auto drop = [&]() {
+      for (int i = 0; i < n; i++)
+        if (done[i]) (void)hipEventDestroy(done[i]);
+    };
     for (int i = 0; i < n; i++) {
       Dev& d = c->devs[i];
-      NCCLCHK(c, ncclGather(d.rec, i == 0 ? root.gather : nullptr, rec_bytes, ncclUint8, 0,
-                            c->comms[i], d.stream));
+      if (hipSetDevice(d.id) != hipSuccess ||
+          hipEventCreateWithFlags(&done[i], hipEventDisableTiming) != hipSuccess ||
+          hipEventRecord(done[i], d.stream) != hipSuccess) {
+        drop();
+        return fail(c, ME_EDEVICE, "device %d: search end event", d.id);
+      }
     }
-    NCCLCHK(c, ncclGroupEnd());
-    // Bounded wait on every device's gather: a device that stalls (or an RCCL
-    // error) aborts the group instead of blocking this call forever; the next
-    // search builds a new one.
+    HIPCHK(c, hipSetDevice(root.id));
+    ncclResult_t r = ncclGroupStart();
+    for (int i = 0; i < n && r == ncclSuccess; i++) {
+      Dev& d = c->devs[i];
+      r = ncclGather(d.rec, i == 0 ? root.gather : nullptr, rec_bytes, ncclUint8, 0, c->comms[i],
+                     d.stream);
+    }
+    const ncclResult_t re = ncclGroupEnd();
+    if (r == ncclSuccess) r = re;
+    if (r != ncclSuccess) {
+      drop();
+      return fail(c, ME_ECOMM, "ncclGather: %s", ncclGetErrorString(r));
+    }
+    // Bounded wait on every device's gather, started once its search is done:
+    // a device that stalls (or an RCCL error) aborts the group instead of
+    // blocking this call forever; the next search builds a new one.
     for (int i = 0; i < n; i++) {
       Dev& d = c->devs[i];
       HIPCHK(c, hipSetDevice(d.id));
-      s = me::wait_comm(c, d.stream, d.search_ev, c->comms[i], ME_COMM_TIMEOUT_MS);
+      const hipError_t e = hipEventSynchronize(done[i]);
+      s = e == hipSuccess ? me::wait_comm(c, d.stream, d.search_ev, c->comms[i], ME_COMM_TIMEOUT_MS)
+                          : fail(c, ME_EDEVICE, "device %d search: %s", d.id, hipGetErrorString(e));
       if (s != ME_OK) {
         for (int k = 0; k < n; k++) (void)ncclCommAbort(c->comms[k]);
         delete[] c->comms;
         c->comms = nullptr;
+        drop();
         return s;
       }
     }
+    drop();
   } else {
     // Repeated device ids: stripes share a device; device copies stand in for the gather.
     for (int i = 0; i < n; i++) {
@@ -554,7 +591,7 @@ const char* me_version(void) { return "me_hip 1 gfx950"; }
 
 void me_set_kernel_path(me_path path) {
   me::set_kernel_path_code(path == ME_PATH_VALU ? 1 : path == ME_PATH_MFMA_TILES ? 2
-                           : path == ME_PATH_MFMA_LEAN ? 3 : 0);
+                           : path == ME_PATH_MFMA_LEAN ? 3 : path == ME_PATH_MFMA_PREPASS ? 4 : 0);
 }
 
 me_status me_create(me_ctx** out, const int* device_ids, int n) {
@@ -590,7 +627,6 @@ me_status me_create(me_ctx** out, const int* device_ids, int n) {
     Dev d;
     d.id = id;
     if (hipSetDevice(id) != hipSuccess ||
-        hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc((void**)&d.sched, me::SCHED_WORDS * 4) != hipSuccess ||
         hipMemset(d.sched, 0, me::SCHED_WORDS * 4) != hipSuccess ||
         hipEventCreateWithFlags(&d.search_ev, hipEventDisableTiming) != hipSuccess) {
@@ -676,6 +712,7 @@ me_status me_device_check(me_ctx* c) {
   (void)hipGetDevice(&prev);
   me_status s = ME_OK;
   for (Dev& d : c->devs) {
+    d.async_unchecked = false;
     uint32_t w = 0;
     if (hipSetDevice(d.id) != hipSuccess ||
         hipMemcpy(&w, d.sched + me::SCHED_ERR, 4, hipMemcpyDeviceToHost) != hipSuccess) {
@@ -739,6 +776,7 @@ me_status me_graph_launch(me_graph* g, void* stream) {
   me_status s = me::order_on(c, d, (hipStream_t)stream);
   if (s != ME_OK) return s;
   HIPCHK(c, hipGraphLaunch(g->exec, (hipStream_t)stream));
+  d.async_unchecked = true;
   return ME_OK;
 }
 
@@ -787,6 +825,7 @@ me_status me_full_search(me_ctx* c, const uint8_t* ref, const uint8_t* cur, int 
     return multi_search(c, ref, cur, width, height, stride, blk, range, cost, mv_xy, block_cost);
   Dev& d = c->devs[0];
   HIPCHK(c, hipSetDevice(d.id));
+  if ((s = me::own_stream(c, d)) != ME_OK) return s;
   const size_t plane = (size_t)width * height;
   const size_t nb = (size_t)me_num_blocks(width, height, blk);
   if ((s = grow(c, (void**)&d.ref, &d.frame_cap, 2 * plane)) != ME_OK) return s;
@@ -824,7 +863,9 @@ me_status me_full_search_stripe_device(me_ctx* c, const uint8_t* d_ref, int ref_
                                range, cost, r0, r1, d_mv, d_cost);
   const bool cap = me::capturing((hipStream_t)stream);
   if ((s = attach_scratch(c, c->devs[0], p, cap)) != ME_OK) return s;
-  return launch_ordered(c, c->devs[0], p, (hipStream_t)stream);
+  if ((s = launch_ordered(c, c->devs[0], p, (hipStream_t)stream)) != ME_OK) return s;
+  c->devs[0].async_unchecked = true;
+  return ME_OK;
 }
 
 me_status me_search_stripes_device(me_ctx* c, int width, int height, int stride, int blk,
@@ -872,7 +913,9 @@ me_status me_search_stripes_device(me_ctx* c, int width, int height, int stride,
     if (s != ME_OK) return s;
   }
   c->err[0] = 0;
-  return me::launch_jobs_ordered(c, d, base, js.data(), n_jobs, (hipStream_t)stream, cap);
+  me_status s = me::launch_jobs_ordered(c, d, base, js.data(), n_jobs, (hipStream_t)stream, cap);
+  if (s == ME_OK) d.async_unchecked = true;
+  return s;
 }
 
 me_status me_full_search_batch_device(me_ctx* c, const uint8_t* d_ref, size_t ref_frame_stride,
@@ -955,6 +998,7 @@ static me_status compensate(me_ctx* c, const uint8_t* ref, const uint8_t* cur, i
   if (!out) return fail(c, ME_EINVAL, "null output");
   Dev& d = c->devs[0];
   HIPCHK(c, hipSetDevice(d.id));
+  if ((s = me::own_stream(c, d)) != ME_OK) return s;
   const size_t plane = (size_t)width * height;
   const size_t nb = (size_t)me_num_blocks(width, height, blk);
   if ((s = grow(c, (void**)&d.ref, &d.frame_cap, 2 * plane)) != ME_OK) return s;

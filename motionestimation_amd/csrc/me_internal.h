@@ -21,7 +21,11 @@ namespace me {
 
 struct Dev {
   int id = 0;
-  hipStream_t stream = nullptr;  // compute stream
+  // The context's own stream, created on first use by the host-plane entry
+  // points (me_full_search, me_search_pairs, me_compensate_planes, ...): a
+  // caller that only uses the device entry points on its own streams never
+  // holds it, so a rank of a multi-process split keeps to its hardware queues.
+  hipStream_t stream = nullptr;
   hipStream_t copy = nullptr;    // upload stream of the pair pipeline (lazy)
   uint8_t* ref = nullptr;        // frame (or stripe) planes, packed pitch = width
   uint8_t* cur = nullptr;
@@ -74,6 +78,10 @@ struct Dev {
   // the device) on behalf of earlier asynchronous searches: me_device_check
   // still reports it once (device_status sets it, me_device_check clears it).
   uint32_t err_pending = 0;
+  // An asynchronous search (a device entry point or a graph launch on a
+  // caller's stream) was enqueued since the last me_device_check: only then
+  // may the invariant word a synchronous call reads belong to another search.
+  bool async_unchecked = false;
 };
 
 // Persistent host workers, one per context device (multi-device searches and
@@ -113,6 +121,8 @@ me_status wait_comm(me_ctx* c, hipStream_t s, hipEvent_t ev, ncclComm_t comm, in
 void release_pipeline(Dev& d);
 
 me_status fail(me_ctx* c, me_status s, const char* fmt, ...);
+// Create d's own stream if it does not exist yet (device d must be current).
+me_status own_stream(me_ctx* c, Dev& d);
 me_status grow(me_ctx* c, void** p, size_t* cap, size_t need);
 me_status check_args(me_ctx* c, const void* ref, const void* cur, int width, int height,
                      int stride, int blk, int range, int cost, const void* mv);

@@ -169,6 +169,16 @@ struct MfmaGeom {
   int* s2h;              // hb x 16 box sums (partial bottom row only)
   unsigned long long* mkeys;  // per tile 16 merge keys (~0 between launches)
   uint32_t* mcnt;        // per tile arrival counters (0 between launches)
+  // Band-walk kernel (me_band.hip, 16x16, the default for S <= 64): a
+  // workgroup walks a strip of block columns down a segment of block rows,
+  // forming each 16-row band's S2 once in LDS for every block row in flight.
+  int bw;                // 1: this plan runs on it (full-height rows [row0, row0 + nrows))
+  int bw_wpc, bw_ns;     // waves per block column (row classes), ring slots per wave
+  int bw_cols;           // block columns per strip (8 / bw_wpc)
+  int bw_strips;         // strips per job
+  int bw_seg_rows;       // block rows per workgroup
+  int bw_segs;           // segments per job
+  int bw_lp, bw_pp;      // window row pitch (bytes), P0 plane row pitch (ints)
 };
 size_t mfma_merge_tiles(const SearchArgs& p);  // tiles the merge buffers must cover
 bool plan_mfma_ssd(const SearchArgs& p, MfmaGeom* g);
@@ -182,6 +192,10 @@ size_t mfma_batch_scratch(const SearchArgs& p, int n);
 // jobs as the scratch holds.  False (nothing launched): not applicable.
 bool launch_mfma_jobs(const SearchArgs& base, const SearchJob* jobs, int n, hipStream_t stream,
                       hipError_t* err);
+// Band-walk kernel (me_band.hip): plan the full-height rows of p into g (g's
+// common fields already set by plan_mfma_ssd), and launch every job of jb.
+bool plan_bw(const SearchArgs& p, MfmaGeom* g, int jobs);
+hipError_t launch_bw(const SearchArgs& p, const MfmaGeom& g, const MfmaJobs& jb, hipStream_t stream);
 // Tiles of cross-workgroup merge buffers (mkeys: 16 u64 keys each, ~0; mcnt:
 // one u32 counter each, 0) the search of p needs (the MFMA SSD kernels).
 size_t merge_tiles_needed(const SearchArgs& p);

@@ -48,6 +48,7 @@
 #include <type_traits>
 
 #include "me_kernels.h"
+#include "me_mfma_util.h"
 #include "me_tuning.h"
 
 // Steps between a row's last MFMA and its epilogue (the 16-register accumulator
@@ -67,7 +68,11 @@ namespace me {
 
 namespace {
 
-typedef int v4i __attribute__((ext_vector_type(4)));
+using mfma::v4i;
+using mfma::opaque;
+using mfma::mfma_job;
+using mfma::umin3;
+using mfma::lshl6_add;
 typedef __attribute__((address_space(3))) const uint32_t lds_u32;
 
 template <int I, int N, typename F>
@@ -98,22 +103,6 @@ __device__ unsigned long long g_pstamps[6 << 14];
 #define PS_STAMP(slot) do { } while (0)
 #endif
 
-__device__ __forceinline__ int opaque(int v) {
-  asm volatile("" : "+v"(v));
-  return v;
-}
-
-// Job j of a batched launch: its planes, records and prepass planes.
-__device__ __forceinline__ void mfma_job(const MfmaJobs& jb, int j, SearchArgs& p, MfmaGeom& g) {
-  p.ref = jb.ref[j];
-  p.cur = jb.cur[j];
-  p.mv = jb.mv[j];
-  p.cost = jb.cost[j];
-  const size_t off = (size_t)j * jb.scratch_stride;
-  g.rp += off;
-  g.s2 = reinterpret_cast<int*>(reinterpret_cast<uint8_t*>(g.s2) + off);
-  if (g.s2h) g.s2h = reinterpret_cast<int*>(reinterpret_cast<uint8_t*>(g.s2h) + off);
-}
 
 // -------------------------------------------------------------- prepass
 // Plane row rr is frame row ya0 + rr; every plane holds rows_alloc rows of
@@ -264,21 +253,9 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, uint8_t* lds_ds
 #ifndef ME_ABL
 #define ME_ABL 0  // diagnostic ablations of the block-major kernel (never in libme_hip.so)
 #endif
-#define MFMA16 __builtin_amdgcn_mfma_i32_16x16x64_i8
-
 __device__ __forceinline__ uint32_t sad_u32(uint32_t a_sgpr, uint32_t b, uint32_t c) {
   uint32_t d;
   asm("v_sad_u32 %0, %1, %2, %3" : "=v"(d) : "s"(a_sgpr), "v"(b), "v"(c));
-  return d;
-}
-__device__ __forceinline__ uint32_t umin3(uint32_t a, uint32_t b, uint32_t c) {
-  uint32_t d;
-  asm("v_min3_u32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
-  return d;
-}
-__device__ __forceinline__ uint32_t lshl6_add(uint32_t a, uint32_t b_sgpr) {
-  uint32_t d;
-  asm("v_lshl_add_u32 %0, %1, 6, %2" : "=v"(d) : "v"(a), "s"(b_sgpr));
   return d;
 }
 
@@ -1820,6 +1797,16 @@ bool plan_mfma_ssd(const SearchArgs& p, MfmaGeom* g) {
   g->rp = reinterpret_cast<int8_t*>(p.scratch);
   g->s2 = p.scratch ? reinterpret_cast<int*>(p.scratch + rp_alloc) : nullptr;
   g->s2h = p.scratch ? reinterpret_cast<int*>(p.scratch + rp_alloc + s2_plane) : nullptr;
+  // Automatic path, S <= 64: the band-walk kernel (me_band.hip) for the
+  // full-height rows, me_mfma_bmv_kernel for a partial bottom row; neither
+  // needs scratch.  ME_PATH_MFMA_PREPASS keeps the prepass + block-major pair.
+  g->bw = 0;
+  if (g->bm && !g->bmv && kernel_path() == 0 && plan_bw(p, g, 1)) {
+    g->bmv_r = 1;
+    g->scratch_bytes = 0;
+    g->rp = nullptr;
+    g->s2 = g->s2h = nullptr;
+  }
   if (g->bmv) {  // no planes: the kernel reads the reference plane
     g->scratch_bytes = 0;
     g->rp = nullptr;
@@ -1848,6 +1835,7 @@ static bool plan_mfma_ssd8(const SearchArgs& p, MfmaGeom* g) {
   g->bm = 0;
   g->bmv = 0;
   g->bmv_r = 1;
+  g->bw = 0;
   g->nbx = W / 8;
   g->tiles_x = (g->nbx + 3) / 4;
   g->tiles_y = (g->nrows + 3) / 4;
@@ -1932,8 +1920,27 @@ static hipError_t launch_bmv(const SearchArgs& p, const MfmaGeom& g, const MfmaJ
   return hipGetLastError();
 }
 
+// The band-walk kernel over the full-height rows of every job of jb, then
+// me_mfma_bmv_kernel over their partial bottom row (if any).
+static hipError_t launch_bw_jobs(const SearchArgs& p, const MfmaGeom& g, const MfmaJobs& jb,
+                                 hipStream_t stream) {
+  hipError_t e = launch_bw(p, g, jb, stream);
+  if (e != hipSuccess || g.hb_row < 0) return e;
+  MfmaGeom t = g;
+  t.bw = 0;
+  t.bmv = 1;
+  t.bmv_r = 1;
+  t.row0 = g.hb_row;
+  t.nrows = 1;
+  t.lds = bmv_lds<1>();
+  MfmaJobs tj = jb;
+  tj.wgs = wgs_per_job(t);
+  return launch_bmv(p, t, tj, stream);
+}
+
 hipError_t launch_mfma_ssd(const SearchArgs& p, const MfmaGeom& g, hipStream_t stream) {
   const MfmaJobs jb = single_job(p, g);
+  if (g.bw) return launch_bw_jobs(p, g, jb, stream);
   if (g.bmv) return launch_bmv(p, g, jb, stream);
   hipError_t e = launch_prep(p, g, jb, stream);
   if (e != hipSuccess) return e;
@@ -1971,7 +1978,7 @@ static size_t batch_stride(const MfmaGeom& g) { return (g.scratch_bytes + 255) &
 // apply (not the block-major kernel, or one job's planes alone exceed the cap).
 static int batch_jobs(const MfmaGeom& g, int n) {
   if (!g.bm || n < 2) return 0;
-  if (g.bmv) return n < MAX_JOBS ? n : MAX_JOBS;  // no prepass planes
+  if (g.bmv || g.bw) return n < MAX_JOBS ? n : MAX_JOBS;  // no prepass planes
   const size_t per = MFMA_BATCH_SCRATCH / batch_stride(g);
   const int m = (int)(per < (size_t)MAX_JOBS ? per : (size_t)MAX_JOBS);
   return m >= 2 ? (n < m ? n : m) : 0;
@@ -1979,7 +1986,7 @@ static int batch_jobs(const MfmaGeom& g, int n) {
 
 size_t mfma_batch_scratch(const SearchArgs& p, int n) {
   MfmaGeom g;
-  if (!plan_mfma_ssd(p, &g) || g.bmv) return 0;
+  if (!plan_mfma_ssd(p, &g) || g.bmv || g.bw) return 0;
   const int m = batch_jobs(g, n);
   return m ? (size_t)m * batch_stride(g) : g.scratch_bytes;
 }
@@ -2008,10 +2015,12 @@ bool launch_mfma_jobs(const SearchArgs& base, const SearchJob* jobs, int n, hipS
   // row loads), else the batch runs job by job, each planned on its own
   for (int i = 1; i < n; i++)
     if ((uintptr_t)jobs[i].ref % 4 || (uintptr_t)jobs[i].cur % (g.bm ? 16 : 4)) return false;
-  const size_t stride = g.bmv ? 0 : batch_stride(g);
+  const bool lean = g.bmv || g.bw;  // no prepass planes
+  const size_t stride = lean ? 0 : batch_stride(g);
   int m = batch_jobs(g, n);
-  if (!g.bmv && (!base.scratch || (m && (size_t)m * stride > base.scratch_bytes)))
+  if (!lean && (!base.scratch || (m && (size_t)m * stride > base.scratch_bytes)))
     m = base.scratch ? (int)(base.scratch_bytes / stride) : 0;
+  if (g.bw) plan_bw(p, &g, m);  // segments sized for m jobs per launch
   if (m < 2 || g.nbx < p.nbx) return false;  // (a partial right column: job by job)
   for (int i0 = 0; i0 < n && *err == hipSuccess; i0 += m) {
     MfmaJobs jb;
@@ -2025,7 +2034,9 @@ bool launch_mfma_jobs(const SearchArgs& base, const SearchJob* jobs, int n, hipS
       jb.mv[j] = J.mv;
       jb.cost[j] = J.cost;
     }
-    if (g.bmv) {
+    if (g.bw) {
+      *err = launch_bw_jobs(p, g, jb, stream);
+    } else if (g.bmv) {
       *err = launch_bmv(p, g, jb, stream);
     } else {
       *err = launch_prep(p, g, jb, stream);

@@ -102,6 +102,8 @@ struct Job {
 
 // Make sure the device's pipeline resources fit this frame size.
 me_status prepare(me_ctx* c, Dev& d, size_t plane) {
+  me_status s0 = own_stream(c, d);
+  if (s0 != ME_OK) return s0;
   if (d.slot_bytes != plane) {  // frame size changed: drop the old slots
     HIPCHK(c, hipStreamSynchronize(d.stream));
     if (d.copy) HIPCHK(c, hipStreamSynchronize(d.copy));
@@ -173,16 +175,27 @@ me_status run_pairs(me_ctx* c, Dev& d, const Job& j, int p0, int p1) {
   if ((s = grow(c, (void**)&d.pair_out, &d.pair_out_cap, np * nb * 8)) != ME_OK) return s;
   int16_t* out_mv = reinterpret_cast<int16_t*>(d.pair_out);
   uint32_t* out_cost = reinterpret_cast<uint32_t*>(d.pair_out + np * nb * 4);
-  if (d.bounce_cap < np * nb * 8) {
+  // Pinned bounce buffer for the records: one region of G pairs per batch
+  // event, indexed by batch mod kEvRing (drain() keeps fewer than kEvRing
+  // batches between download and drain, so a region is free again when its
+  // batch index comes round): at most kEvRing * G pairs pinned, whatever the
+  // length of the pair list.
+  const int G = tuning().stream_batch > 0 ? tuning().stream_batch : kPairBatch;
+  const size_t region = (size_t)G * nb * 8;  // [G * nb mv (4 B)][G * nb cost (4 B)]
+  const size_t bneed = region * (size_t)std::min<size_t>(kEvRing, (np + G - 1) / G + 4);
+  if (d.bounce_cap < bneed) {
     if (d.bounce) (void)hipHostFree(d.bounce);
     d.bounce = nullptr;
     d.bounce_cap = 0;
-    if (hipHostMalloc((void**)&d.bounce, np * nb * 8, hipHostMallocDefault) != hipSuccess)
-      return fail(c, ME_ENOMEM, "pinned record buffer of %zu bytes failed", np * nb * 8);
-    d.bounce_cap = np * nb * 8;
+    if (hipHostMalloc((void**)&d.bounce, bneed, hipHostMallocDefault) != hipSuccess)
+      return fail(c, ME_ENOMEM, "pinned record buffer of %zu bytes failed", bneed);
+    d.bounce_cap = bneed;
   }
-  int16_t* bnc_mv = reinterpret_cast<int16_t*>(d.bounce);
-  uint32_t* bnc_cost = reinterpret_cast<uint32_t*>(d.bounce + np * nb * 4);
+  const size_t nregions = d.bounce_cap / region;
+  auto bnc_mv = [&](int b) { return reinterpret_cast<int16_t*>(d.bounce + (size_t)(b % nregions) * region); };
+  auto bnc_cost = [&](int b) {
+    return reinterpret_cast<uint32_t*>(d.bounce + (size_t)(b % nregions) * region + region / 2);
+  };
   // Records of batch b leave on the copy stream, queued behind batch b + 1's
   // uploads (which must overlap batch b's search) and ahead of batch b + 2's
   // (which the host enqueues only after batch b is done anyway).  A stream of
@@ -200,9 +213,9 @@ me_status run_pairs(me_ctx* c, Dev& d, const Job& j, int p0, int p1) {
     const size_t o = (size_t)(ranges[b].first - p0) * nb;
     const size_t k = (size_t)(ranges[b].second - ranges[b].first) * nb;
     HIPCHK(c, hipStreamWaitEvent(dl, d.batch_ev[b % kEvRing], 0));
-    HIPCHK(c, hipMemcpyAsync(bnc_mv + 2 * o, out_mv + 2 * o, k * 4, hipMemcpyDeviceToHost, dl));
+    HIPCHK(c, hipMemcpyAsync(bnc_mv(b), out_mv + 2 * o, k * 4, hipMemcpyDeviceToHost, dl));
     if (j.block_cost)
-      HIPCHK(c, hipMemcpyAsync(bnc_cost + o, out_cost + o, k * 4, hipMemcpyDeviceToHost, dl));
+      HIPCHK(c, hipMemcpyAsync(bnc_cost(b), out_cost + o, k * 4, hipMemcpyDeviceToHost, dl));
     HIPCHK(c, hipEventRecord(d.d2h_ev[b % kEvRing], dl));
     return ME_OK;
   };
@@ -213,8 +226,8 @@ me_status run_pairs(me_ctx* c, Dev& d, const Job& j, int p0, int p1) {
       HIPCHK(c, hipEventSynchronize(d.d2h_ev[drained % kEvRing]));
       const size_t o = (size_t)(ranges[drained].first - p0) * nb;
       const size_t k = (size_t)(ranges[drained].second - ranges[drained].first) * nb;
-      memcpy(j.mv_xy + 2 * nb * p0 + 2 * o, bnc_mv + 2 * o, k * 4);
-      if (j.block_cost) memcpy(j.block_cost + nb * p0 + o, bnc_cost + o, k * 4);
+      memcpy(j.mv_xy + 2 * nb * p0 + 2 * o, bnc_mv(drained), k * 4);
+      if (j.block_cost) memcpy(j.block_cost + nb * p0 + o, bnc_cost(drained), k * 4);
     }
     return ME_OK;
   };
@@ -251,7 +264,6 @@ me_status run_pairs(me_ctx* c, Dev& d, const Job& j, int p0, int p1) {
   // launches), so a launch's fill and drain are paid once per G pairs.  The
   // slots a batch frees cool while the next batch's frames upload into older
   // ones: at least G + 1 of them.
-  const int G = tuning().stream_batch > 0 ? tuning().stream_batch : kPairBatch;
   const size_t cool = (size_t)std::max(cooling_slots(), G + 1);
   // Ordering events: one per batch on each stream, not one per frame slot.
   // The round-3 scheme (a ready event per upload, a free event per released

@@ -37,6 +37,8 @@ struct Tuning {
   int item_batch = -1;    // ME_ITEM_BATCH=0: item-kernel jobs launch one by one (diagnostic)
   int ahead = -1;         // ME_AHEAD=1|2: item-kernel tiles claimed ahead (-1 = automatic)
   int strip = -1;         // ME_STRIP=0..64: item-kernel tile strips (0 = row-major; -1 = automatic)
+  int bw = -1;            // ME_BW=0|1: 16x16 SSD band-walk kernel off / on where it applies (-1 = automatic: on)
+  int bw_seg = 0;         // ME_BW_SEG=1..4096: band-walk block rows per workgroup (0 = automatic)
 };
 
 const Tuning& tuning();

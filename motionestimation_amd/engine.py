@@ -51,7 +51,7 @@ def set_kernel_path(path: str) -> None:
     (S <= 64) forming S2 in the search kernel (no prepass planes, no scratch).
     Process-wide; results are identical."""
     codes = {"auto": _lib.ME_PATH_AUTO, "valu": _lib.ME_PATH_VALU, "tiles": _lib.ME_PATH_MFMA_TILES,
-             "lean": _lib.ME_PATH_MFMA_LEAN}
+             "lean": _lib.ME_PATH_MFMA_LEAN, "prepass": _lib.ME_PATH_MFMA_PREPASS}
     if path not in codes:
         raise MEError(_lib.ME_EINVAL, f"unknown kernel path {path!r}")
     _lib.lib().me_set_kernel_path(codes[path])

@@ -1,6 +1,8 @@
-"""Matrix-core SSD path (me_mfma.hip: i8 MFMA cross term + S2 prepass, or S2
-formed in the search kernel on the lean path) against the oracle and against
-the VALU kernels, bit-exact (MVs and integer SSDs).
+"""Matrix-core SSD path (i8 MFMA cross term; the S2 term formed per band in
+the band-walk kernel on the automatic path (me_band.hip), per workgroup on the
+lean path, or read from a prepass plane on the prepass path (me_mfma.hip))
+against the oracle and against the VALU kernels, bit-exact (MVs and integer
+SSDs).
 
 The MFMA path serves B = 16 SSD on full blocks; tiles of 4x4 blocks, chunks of
 L = 45/61 candidate rows, 1-4 groups of 64 candidate columns (S up to 103).
@@ -22,11 +24,12 @@ pytestmark = pytest.mark.gpu
 NT = min(16, os.cpu_count() or 1)
 
 
-@pytest.fixture(params=["auto", "lean"], autouse=True)
+@pytest.fixture(params=["auto", "lean", "prepass"], autouse=True)
 def ssd_path(request):
-    """Every case on the default matrix-core path (prepass planes) and on the
-    lean one (ME_PATH_MFMA_LEAN: 16x16, S <= 64 forms S2 in the search kernel;
-    other shapes plan as auto).  Cases that switch paths themselves end on auto."""
+    """Every case on the default matrix-core path (16x16, S <= 64: the
+    band-walk kernel), on the lean one (ME_PATH_MFMA_LEAN: S2 per workgroup)
+    and on the prepass one (ME_PATH_MFMA_PREPASS: S2 planes); other shapes plan
+    as auto.  Cases that switch paths themselves end on auto."""
     me.set_kernel_path(request.param)
     yield request.param
     me.set_kernel_path("auto")
@@ -283,3 +286,71 @@ def test_mfma_batch_mixed_alignment(engine):
         omv, oco, _ = O.full_search(r, c, blk, span, "ssd", threads=NT)
         np.testing.assert_array_equal(mv.cpu().numpy(), omv, err_msg=f"job {f}")
         np.testing.assert_array_equal(co.cpu().numpy().view(np.uint32), oco, err_msg=f"job {f}")
+
+
+@pytest.mark.parametrize("shape,span", [((720, 1280), 32), ((544, 960), 16), ((368, 656), 64),
+                                        ((1080, 1920), 32)])
+def test_band_walk_segments_and_batches(engine, ssd_path, shape, span):
+    """The band-walk kernel splits a frame into segments of block rows when
+    its strips alone do not fill the CUs (single frames) and walks whole
+    strips in batches: one frame, and the same frame in a batch of 6 with
+    other frames, against the oracle (partial bottom rows: 368 = 23 x 16,
+    1080 = 67 x 16 + 8, handed to the lean kernel)."""
+    import torch
+    if ssd_path != "auto":
+        pytest.skip("band-walk geometry: automatic path only")
+    h, w = shape
+    rng = np.random.default_rng(h + span)
+    pairs = [_pair(rng, h, w, dx=int(rng.integers(-5, 6)), dy=int(rng.integers(-5, 6))) for _ in range(6)]
+    ref, cur = pairs[0]
+    _check(engine, ref, cur, span, f"{h}x{w} S{span} single")
+    dev = torch.device("cuda", 0)
+    nb = me.num_blocks(w, h, 16)
+    rt = torch.from_numpy(np.stack([r for r, _ in pairs])).to(dev)
+    ct = torch.from_numpy(np.stack([c for _, c in pairs])).to(dev)
+    mv = torch.empty((6 * nb, 2), dtype=torch.int16, device=dev)
+    co = torch.empty(6 * nb, dtype=torch.int32, device=dev)
+    engine.search_batch_device(rt, 0, ct, 0, w, h, 16, span, "ssd", 0, (h + 15) // 16, mv, co)
+    torch.cuda.synchronize()
+    mv, co = mv.cpu().numpy().reshape(6, nb, 2), co.cpu().numpy().view(np.uint32).reshape(6, nb)
+    for f, (r, c) in enumerate(pairs):
+        omv, oc, _ = O.full_search(r, c, 16, span, "ssd", threads=NT)
+        np.testing.assert_array_equal(mv[f], omv, err_msg=f"frame {f}")
+        np.testing.assert_array_equal(co[f], oc, err_msg=f"frame {f}")
+
+
+_SEG_SCRIPT = r"""
+import sys
+sys.path.insert(0, {repo!r}); sys.path.insert(0, {tests!r})
+import numpy as np
+import motionestimation_amd as me
+from motionestimation_amd import synth
+import oracle_lib as O
+assert me._lib.LIB_PATH.endswith("libme_hip_tune.so"), me._lib.LIB_PATH
+rng = np.random.default_rng(5)
+with me.Engine() as eng:
+    for (h, w, span) in [(400, 480, 32), (336, 272, 7), (304, 400, 48)]:
+        ref = synth._box5(rng.integers(0, 256, (h, w), dtype=np.uint8))
+        cur = synth.shift_plane(ref, 3, -2)
+        mv, c = eng.full_search(ref, cur, 16, span, "ssd")
+        omv, oc, _ = O.full_search(ref, cur, 16, span, "ssd")
+        assert np.array_equal(mv, omv) and np.array_equal(c, oc), (h, w, span)
+print("segments ok")
+"""
+
+
+@pytest.mark.parametrize("seg", [1, 2, 3, 5, 7])
+def test_band_walk_forced_segment_rows(tmp_path, seg):
+    """The tuning build with ME_BW_SEG: segments of 1, 2, 3, 5 and 7 block
+    rows (every boundary a prologue re-forms the bands above it), S 7 / 32 / 48."""
+    import subprocess
+    import sys
+    lib = os.path.join(O.REPO, "motionestimation_amd", "lib", "libme_hip_tune.so")
+    assert os.path.exists(lib), "build with __graft_entry__.build()"
+    script = tmp_path / "seg.py"
+    script.write_text(_SEG_SCRIPT.format(repo=O.REPO, tests=os.path.join(O.REPO, "tests")))
+    env = dict(os.environ, ME_HIP_LIB="libme_hip_tune.so", ME_BW_SEG=str(seg))
+    r = subprocess.run([sys.executable, str(script)], capture_output=True, text=True, timeout=300,
+                       env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "segments ok" in r.stdout

@@ -227,6 +227,51 @@ def test_bench_stripe_mode_rccl_one_rank():
     assert "me_gather_device" in d["stripe_4k"]["gather"]
 
 
+def _live_streams(log):
+    """Streams a process had created and not destroyed while its search
+    kernels were launched (the most at any such launch), from the HIP
+    runtime's own API log (AMD_LOG_LEVEL=3): creations return 'stream:0x...',
+    destructions name it, launches log 'ShaderName : <kernel>'.  (RCCL's proxy
+    thread creates and destroys one more stream during communicator setup,
+    before any search.)"""
+    import re
+    live, peak = set(), 0
+    for line in log.splitlines():
+        m = re.search(r"hipStreamCreate\w*: Returned hipSuccess : stream:(0x[0-9a-f]+)", line)
+        if m:
+            live.add(m.group(1))
+            continue
+        m = re.search(r"hipStreamDestroy \( stream:(0x[0-9a-f]+)", line)
+        if m:
+            live.discard(m.group(1))
+            continue
+        if "ShaderName : " in line and "me::" in line:
+            peak = max(peak, len(live))
+    return peak
+
+
+def test_rccl_rank_stream_budget():
+    """A bench.py RCCL stripe rank holds at most 4 created HIP streams
+    (GPU_MAX_HW_QUEUES = 4 hardware queues per process): torch's stream (the
+    searches and the gather) and the one RCCL communicator's (the library's
+    ncclGather).  The library creates none for device entry points (its own
+    stream is lazy), and torch's process group is gloo (the control plane), so
+    there is no second communicator (round 4: torch's "nccl" group + the
+    library's communicator + the context stream).  Counted from the HIP
+    runtime's API log of the one-rank run."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr=127.0.0.1", "--master-port=29733", os.path.join(O.REPO, "bench.py"),
+           "--gpus", "1", "--mode", "stripe", "--steps", "3", "--warmup", "1", "--no-cpu",
+           "--no-4k", "--ramp-ms", "5"]
+    env = dict(os.environ, OMP_NUM_THREADS="1", AMD_LOG_LEVEL="3")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=115, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert "me_gather_device" in d["config"]["gather"]
+    peak = _live_streams(r.stderr)
+    assert 1 <= peak <= 4, f"{peak} live streams"
+
+
 @pytest.mark.skipif("_ngpu() < 2", reason="needs >= 2 GPUs (one RCCL rank per GPU)")
 def test_bench_stripe_mode_rccl():
     """The same over RCCL, one rank per GPU (asynchronous gathers overlapping

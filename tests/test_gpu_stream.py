@@ -151,3 +151,91 @@ def test_seq_driver_foreman_i420(tmp_path, manifest):
     for k, name in enumerate(["foreman21_b8_s12", "foreman41_b8_s12"]):
         gmv, _ = O.load_case(_case(manifest, name))
         np.testing.assert_array_equal(mv[k].astype(np.int32), gmv, err_msg=name)
+
+
+def _long_pair_list(n_frames):
+    """> 16 batches of the 1, 2, 3, 4, 6, 8 ramp: consecutive pairs, (f, f)
+    pairs, backwards pairs and frame 0 reused after a long gap (its slot was
+    freed and reused meanwhile), so the batch-event ring and the record bounce
+    regions wrap and slots are reused after their last reader's event slot was
+    overwritten."""
+    pairs = []
+    for k in range(n_frames - 1):
+        pairs.append((k, k + 1))
+        if k % 7 == 3:
+            pairs.append((k, k))
+        if k % 11 == 5:
+            pairs.append((k + 1, k - 2))
+    pairs.append((0, n_frames - 1))
+    pairs.append((n_frames - 1, 0))
+    return pairs
+
+
+def _check_pairs(seq, pairs, mv, c, blk, rng, cost):
+    for k, (r, q) in enumerate(pairs):
+        omv, oc, _ = O.full_search(seq[r], seq[q], blk, rng, cost, threads=1)
+        np.testing.assert_array_equal(mv[k], omv, err_msg=f"pair {k} ({r}, {q})")
+        np.testing.assert_array_equal(c[k], oc, err_msg=f"pair {k} ({r}, {q})")
+
+
+@pytest.mark.parametrize("pinned", [False, True])
+def test_long_pair_list_ring_wrap(engine, pinned):
+    """>= 150 small pairs (> 16 batches): every record against the oracle, from
+    pageable and from me_host_alloc frames (the event ring, the
+    bounce-region ring, the drain bound and slot reuse had no result check)."""
+    w, h, n = 64, 48, 130
+    seq = synth.sequence(w, h, n, 21, 1, -1)
+    pairs = _long_pair_list(n)
+    assert len(pairs) >= 150
+    frames = list(seq)
+    if pinned:
+        buf = me.pinned_frames(n, h, w)
+        buf[:] = seq
+        frames = list(buf)
+    mv, c = engine.search_pairs(frames, pairs, 8, 7, "sad")
+    _check_pairs(seq, pairs, mv, c, 8, 7, "sad")
+    # and again on the same context (slots, events and bounce regions reused)
+    mv2, c2 = engine.search_pairs(frames, pairs[::-1], 8, 7, "sad")
+    np.testing.assert_array_equal(mv2[::-1], mv)
+    np.testing.assert_array_equal(c2[::-1], c)
+
+
+_TUNE_SCRIPT = r"""
+import sys
+sys.path.insert(0, {repo!r}); sys.path.insert(0, {tests!r})
+import numpy as np
+import motionestimation_amd as me
+from motionestimation_amd import synth
+import oracle_lib as O
+from test_gpu_stream import _long_pair_list, _check_pairs
+assert me._lib.LIB_PATH.endswith("libme_hip_tune.so"), me._lib.LIB_PATH
+w, h, n = 64, 48, 130
+seq = synth.sequence(w, h, n, 21, 1, -1)
+pairs = _long_pair_list(n)
+with me.Engine() as eng:
+    for pinned in (False, True):
+        frames = list(seq)
+        if pinned:
+            buf = me.pinned_frames(n, h, w); buf[:] = seq; frames = list(buf)
+        mv, c = eng.search_pairs(frames, pairs, 8, 7, "ssd")
+        _check_pairs(seq, pairs, mv, c, 8, 7, "ssd")
+print("tuned pipeline ok", len(pairs))
+"""
+
+
+def test_long_pair_list_unbounded_ahead_fixed_batches(tmp_path):
+    """The tuning build with ME_STREAM_AHEAD=9 (host unbounded ahead of the
+    GPU) and ME_STREAM_RAMP=0 (fixed 8-pair batches): the same long pair list,
+    SSD, pinned and pageable, every pair against the oracle."""
+    import os
+    import subprocess
+    import sys
+    lib = os.path.join(O.REPO, "motionestimation_amd", "lib", "libme_hip_tune.so")
+    assert os.path.exists(lib), "build with __graft_entry__.build()"
+    script = tmp_path / "tuned.py"
+    script.write_text(_TUNE_SCRIPT.format(repo=O.REPO, tests=os.path.join(O.REPO, "tests")))
+    env = dict(os.environ, ME_HIP_LIB="libme_hip_tune.so", ME_STREAM_AHEAD="9", ME_STREAM_RAMP="0")
+    r = subprocess.run([sys.executable, str(script)], capture_output=True, text=True, timeout=300,
+                       env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "tuned pipeline ok" in r.stdout
