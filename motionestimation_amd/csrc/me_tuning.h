@@ -39,6 +39,8 @@ struct Tuning {
   int strip = -1;         // ME_STRIP=0..64: item-kernel tile strips (0 = row-major; -1 = automatic)
   int bw = -1;            // ME_BW=0|1: 16x16 SSD band-walk kernel off / on where it applies (-1 = automatic: on)
   int bw_seg = 0;         // ME_BW_SEG=1..4096: band-walk block rows per workgroup (0 = automatic)
+  int bw_abl = 0;         // ME_BW_ABL=0..15: band-walk ablations, timing only (results invalid):
+                          // 1 no production, 2 no tiles, 4 no row entries, 8 no XOR pass
 };
 
 const Tuning& tuning();
