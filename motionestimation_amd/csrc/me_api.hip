@@ -65,6 +65,7 @@ static Tuning read_tuning() {
   env_int("ME_STREAM_BATCH", 1, 32, &t.stream_batch);
   env_int("ME_STREAM_RAMP", 0, 1, &t.stream_ramp);
   env_int("ME_STREAM_D2H", 0, 1, &t.stream_d2h);
+  env_int("ME_STREAM_CPY", 1, 16, &t.stream_cpy);
   env_int("ME_FLOW", 0, 1, &t.flow);
   env_int("ME_FLOW_SLOTS", 2, 16, &t.flow_slots);
   env_int("ME_PRIO", 0, 1, &t.prio);
@@ -78,7 +79,7 @@ static Tuning read_tuning() {
   env_int("ME_MFMA_S2R", 1, 2, &t.mfma_s2r);
   env_int("ME_BW", 0, 1, &t.bw);
   env_int("ME_BW_SEG", 1, 4096, &t.bw_seg);
-  env_int("ME_BW_ABL", 0, 15, &t.bw_abl);
+  env_int("ME_BW_ABL", 0, 63, &t.bw_abl);
   if (const char* e = getenv("ME_FAIR_T")) {
     int lo = 0, hi = 0;
     if (sscanf(e, "%d,%d", &lo, &hi) == 2 && lo >= 1 && lo <= hi && hi <= 255) {
@@ -333,7 +334,7 @@ void Workers::loop(int i) {
   unsigned long long seen = 0;
   for (;;) {
     const std::function<void(int)>* fn;
-    int n;
+    int n, off;
     {
       std::unique_lock<std::mutex> lk(mu_);
       go_.wait(lk, [&] { return stop_ || gen_ != seen; });
@@ -341,8 +342,9 @@ void Workers::loop(int i) {
       seen = gen_;
       fn = fn_;
       n = n_;
+      off = off_;
     }
-    if (i < n) (*fn)(i);
+    if (i < n) (*fn)(i + off);
     {
       std::lock_guard<std::mutex> lk(mu_);
       if (--pending_ == 0) done_.notify_one();
@@ -354,9 +356,26 @@ void Workers::run(int n, const std::function<void(int)>& fn) {
   std::unique_lock<std::mutex> lk(mu_);
   fn_ = &fn;
   n_ = n;
+  off_ = 0;
   pending_ = (int)th_.size();
   gen_++;
   go_.notify_all();
+  done_.wait(lk, [&] { return pending_ == 0; });
+  fn_ = nullptr;
+}
+
+void Workers::run_split(int n, const std::function<void(int)>& fn) {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    fn_ = &fn;
+    n_ = n - 1;
+    off_ = 1;
+    pending_ = (int)th_.size();
+    gen_++;
+  }
+  go_.notify_all();
+  fn(0);
+  std::unique_lock<std::mutex> lk(mu_);
   done_.wait(lk, [&] { return pending_ == 0; });
   fn_ = nullptr;
 }

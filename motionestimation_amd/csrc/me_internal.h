@@ -19,6 +19,8 @@
 
 namespace me {
 
+class Workers;
+
 struct Dev {
   int id = 0;
   // The context's own stream, created on first use by the host-plane entry
@@ -58,6 +60,7 @@ struct Dev {
   uint8_t* stage[2] = {nullptr, nullptr};  // pinned staging for pageable frames
   hipEvent_t stage_ev[2] = {nullptr, nullptr};
   size_t stage_bytes = 0;
+  Workers* stage_pool = nullptr;  // helper threads of the staging copy (run_pairs)
   // One event pair per batch of pairs (ring by batch index): the batch's uploads
   // done (copy stream; the compute stream waits on it once) and its search done
   // (compute stream; bounds the host's run-ahead and guards slot reuse).
@@ -94,6 +97,8 @@ class Workers {
   ~Workers();
   int size() const { return (int)th_.size(); }
   void run(int n, const std::function<void(int)>& fn);
+  // fn(0) on the calling thread, fn(1 .. n - 1) on workers 0 .. n - 2
+  void run_split(int n, const std::function<void(int)>& fn);
 
  private:
   void loop(int i);
@@ -102,7 +107,7 @@ class Workers {
   std::condition_variable go_, done_;
   const std::function<void(int)>* fn_ = nullptr;
   unsigned long long gen_ = 0;
-  int n_ = 0, pending_ = 0;
+  int n_ = 0, off_ = 0, pending_ = 0;
   bool stop_ = false;
 };
 

@@ -83,6 +83,8 @@ void release_pipeline(Dev& d) {
     d.stage_ev[k] = nullptr;
   }
   d.stage_bytes = 0;
+  delete d.stage_pool;
+  d.stage_pool = nullptr;
   (void)hipFree(d.pair_out);
   d.pair_out = nullptr;
   d.pair_out_cap = 0;
@@ -317,11 +319,27 @@ me_status run_pairs(me_ctx* c, Dev& d, const Job& j, int p0, int p1) {
           // the copy that last read this staging buffer must be done
           HIPCHK(c, hipEventSynchronize(d.stage_ev[stage_k]));
           uint8_t* st = d.stage[stage_k];
-          if (j.stride == W) {
-            memcpy(st, src, plane);
-          } else {
-            for (int y = 0; y < H; y++) memcpy(st + (size_t)y * W, src + (size_t)y * j.stride, W);
+          // The copy into staging is host-memory-bound on one thread (a 1080p
+          // frame ~80 us, more than a pair's search): split it over the caller
+          // and kCpy - 1 helper threads.
+          auto copy_rows = [&](int y0, int y1) {
+            if (j.stride == W)
+              memcpy(st + (size_t)y0 * W, src + (size_t)y0 * W, (size_t)(y1 - y0) * W);
+            else
+              for (int y = y0; y < y1; y++) memcpy(st + (size_t)y * W, src + (size_t)y * j.stride, W);
+          };
+          const int kCpy = std::min(tuning().stream_cpy > 0 ? tuning().stream_cpy : 4, std::max(1, H / 64));
+          if (kCpy > 1 && !d.stage_pool) {
+            try {
+              d.stage_pool = new Workers(kCpy - 1);
+            } catch (...) {  // no thread could be started: copy on this thread
+              d.stage_pool = nullptr;
+            }
           }
+          if (kCpy > 1 && d.stage_pool && d.stage_pool->size() + 1 >= kCpy)
+            d.stage_pool->run_split(kCpy, [&](int i) { copy_rows(H * i / kCpy, H * (i + 1) / kCpy); });
+          else
+            copy_rows(0, H);
           if ((s = upload_pinned(c, d, d.slots[si], st, W, H, W)) != ME_OK) return s;
           HIPCHK(c, hipEventRecord(d.stage_ev[stage_k], d.copy));
           stage_k ^= 1;

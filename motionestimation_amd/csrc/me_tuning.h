@@ -22,6 +22,7 @@ struct Tuning {
   int stream_ahead = 0;   // ME_STREAM_AHEAD=1..9: host run-ahead (9: unbounded; 0 = automatic)
   int stream_batch = 0;   // ME_STREAM_BATCH=1..32: pairs per search launch after the ramp (0 = automatic)
   int stream_d2h = 0;     // ME_STREAM_D2H=1: pair records download on a stream of their own
+  int stream_cpy = 0;     // ME_STREAM_CPY=1..16: threads of a pageable frame's staging copy (0 = 4)
   int stream_ramp = -1;   // ME_STREAM_RAMP=0: no ramp, every launch ME_STREAM_BATCH pairs (-1 = ramp)
   int flow = -1;          // ME_FLOW=0|1: SAD flow kernel off / allowed (-1 = automatic)
   int flow_slots = 0;     // ME_FLOW_SLOTS=2..16: flow kernel LDS ring slots (0 = automatic)
@@ -39,8 +40,10 @@ struct Tuning {
   int strip = -1;         // ME_STRIP=0..64: item-kernel tile strips (0 = row-major; -1 = automatic)
   int bw = -1;            // ME_BW=0|1: 16x16 SSD band-walk kernel off / on where it applies (-1 = automatic: on)
   int bw_seg = 0;         // ME_BW_SEG=1..4096: band-walk block rows per workgroup (0 = automatic)
-  int bw_abl = 0;         // ME_BW_ABL=0..15: band-walk ablations, timing only (results invalid):
-                          // 1 no production, 2 no tiles, 4 no row entries, 8 no XOR pass
+  int bw_abl = 0;         // ME_BW_ABL=0..63: band-walk ablations, timing only (results invalid):
+                          // 1 no production, 2 no tiles, 4 no row entries, 8 no XOR pass;
+                          // variants (results valid): 16 producer waves at raised priority,
+                          // 32 searcher waves at raised priority
 };
 
 const Tuning& tuning();
