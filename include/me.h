@@ -115,6 +115,22 @@ typedef enum {
 } me_path;
 void me_set_kernel_path(me_path path);
 
+/* The kernel family that ran the most recent search launched in this process
+ * (any context, any thread; diagnostics and tests, e.g. that the AUTO path of
+ * a 16x16 SSD search is the band-walk kernel).  The matrix-core SSD kernels
+ * report the kernel of the frame's full-height block rows. */
+typedef enum {
+  ME_SEARCH_PATH_NONE = 0,           /* no search launched yet */
+  ME_SEARCH_PATH_VALU = 1,           /* SAD and SSD VALU kernels (flow, item, generic) */
+  ME_SEARCH_PATH_MFMA_PREPASS = 2,   /* S2 prepass + block-major MFMA kernel */
+  ME_SEARCH_PATH_MFMA_BANDWALK = 3,  /* band-walk MFMA kernel (me_band.hip) */
+  ME_SEARCH_PATH_MFMA_LEAN = 4,      /* per-workgroup S2 MFMA kernel (bmv) */
+  ME_SEARCH_PATH_MFMA_TILES = 5,     /* 4x4-block-tile MFMA kernel */
+  ME_SEARCH_PATH_MFMA_8X8 = 6,       /* 8x8-block MFMA kernel */
+  ME_SEARCH_PATH_SSIM = 7            /* SSIM kernels */
+} me_search_path;
+int me_last_search_path(void);
+
 /* Tiling helpers (src/common/prediction_frame.c:9-11). */
 int me_num_blocks(int width, int height, int block_size);
 /* Exact number of candidates the search evaluates (reference clamping). */

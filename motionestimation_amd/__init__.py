@@ -8,7 +8,7 @@ interface over that ABI.  There is no CPU fallback.
 from ._lib import (ME_COST_SAD, ME_COST_SSD, ME_COST_SSIM, ME_ECOMM, ME_EDEVICE,  # noqa: F401
                    MEError, build)
 from .engine import (Engine, candidate_count, num_blocks, pinned_frames,  # noqa: F401
-                     plan_stripes, set_kernel_path, version)
+                     last_search_path, plan_stripes, set_kernel_path, version)
 from . import io  # noqa: F401
 from .reference_api import (Block, PredictionFrame, create_prediction_frame,  # noqa: F401
                             find_best_blk_mse, find_best_blk_ssim, find_best_blks,

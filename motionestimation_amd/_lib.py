@@ -34,6 +34,7 @@ _SIGS = {
     "me_version": (ctypes.c_char_p, []),
     "me_num_blocks": (ctypes.c_int, [ctypes.c_int] * 3),
     "me_set_kernel_path": (None, [ctypes.c_int]),
+    "me_last_search_path": (ctypes.c_int, []),
     "me_candidate_count": (ctypes.c_uint64, [ctypes.c_int] * 4),
     "me_full_search": (ctypes.c_int, [ctypes.c_void_p, _u8p, _u8p] + [ctypes.c_int] * 6 +
                        [ctypes.c_void_p, ctypes.c_void_p]),

@@ -79,7 +79,8 @@ static Tuning read_tuning() {
   env_int("ME_MFMA_S2R", 1, 2, &t.mfma_s2r);
   env_int("ME_BW", 0, 1, &t.bw);
   env_int("ME_BW_SEG", 1, 4096, &t.bw_seg);
-  env_int("ME_BW_ABL", 0, 63, &t.bw_abl);
+  env_int("ME_BW_WG", 1, 2, &t.bw_wg);
+  env_int("ME_BW_ABL", 0, 1023, &t.bw_abl);
   if (const char* e = getenv("ME_FAIR_T")) {
     int lo = 0, hi = 0;
     if (sscanf(e, "%d,%d", &lo, &hi) == 2 && lo >= 1 && lo <= hi && hi <= 255) {
@@ -608,6 +609,8 @@ const char* me_status_str(me_status s) {
 const char* me_last_error(const me_ctx* ctx) { return ctx ? ctx->err : "null context"; }
 
 const char* me_version(void) { return "me_hip 1 gfx950"; }
+
+int me_last_search_path(void) { return me::last_path(); }
 
 void me_set_kernel_path(me_path path) {
   me::set_kernel_path_code(path == ME_PATH_VALU ? 1 : path == ME_PATH_MFMA_TILES ? 2

@@ -17,25 +17,28 @@
 // band and leaves after its last, so the A fragments of the rows in flight
 // stay in registers (a ring of NS slots per searcher wave).
 //
-//   waves      8 (512 threads, one workgroup per CU), two roles, one of each
-//              per SIMD (waves w and w + 4 share SIMD w):
-//   searchers  waves 0..3: block column w % C of the strip, row class w / C
-//              (4 / C classes split a column's rows in flight).  Per band and
-//              tile: 8 B fragments (ds_read_b128, two fragments ahead) and one
-//              P0 vector; 8 MFMAs per row in flight, the rows interleaved
-//              (independent accumulation chains); keys as the block-major
-//              kernel's.  Nothing else but the rows' entries and exits.
-//   producers  waves 4..7: the window slabs (LDS DMA), the XOR-ed copy, and
-//              S2: band m is produced by producer (m - first band) % 4 during
-//              the 4 iterations before it is searched (46 steps of a sliding
-//              16-row sum, 12 per iteration), lane = 4 positions (one v_dot4
-//              per window row of 4 bytes), the 16-wide horizontal sum by DPP
+//   waves      16 (1,024 threads, one workgroup per CU, <= 128 VGPRs), two
+//              roles: three searchers and one producer per SIMD.
+//   searchers  waves 0..11: block column w % C of the strip, row class w / C
+//              (12 / C classes split a column's rows in flight, two ring slots
+//              each: A fragments of 2 rows = 64 VGPRs).  Per band and tile: 8 B
+//              fragments (ds_read_b128, two fragments ahead) and one P0
+//              vector; 8 MFMAs per row in flight, the rows interleaved
+//              (independent accumulation chains), no MFMA for a free slot;
+//              keys as the block-major kernel's.  Nothing else but the rows'
+//              entries and exits.
+//   producers  waves 12..15: the window slabs (LDS DMA) and S2: band m is
+//              produced by producer (m - first band) % 4 during the 4
+//              iterations before it is searched (46 steps of a sliding 16-row
+//              sum, 12 per iteration), lane = 4 positions (one v_dot4 per
+//              window row of 4 bytes), the 16-wide horizontal sum by DPP
 //              within 16-lane rows, the result stored as the key's position
-//              term P0 = (S2 << 6) + 2^29 + 64 + (x & 3).  Their VALU work
-//              runs beside the searchers' MFMAs on the same SIMDs.
+//              term P0 = (S2 << 6) + 2^29 + 64 + (x & 3); the first 16 steps
+//              also store slab m XOR-ed with 0x80.  Their VALU work runs beside
+//              the searchers' MFMAs on the same SIMDs.
 //   LDS        the window in 16-row slabs: a raw ring (6 slabs ahead) read by
 //              the producers, and the slabs XOR-ed with 0x80 (the MFMA B
-//              operand r - 128) in a ring of 3 + a mirror of slot 0, so a
+//              operand r - 128) in a ring of 5 + a mirror of slot 0, so a
 //              band's 31 rows are contiguous; 5 P0 planes (the band searched +
 //              the 4 in production)
 //
@@ -50,6 +53,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "me_kernels.h"
 #include "me_mfma_util.h"
@@ -65,13 +69,19 @@ using mfma::mfma_job;
 using mfma::opaque;
 using mfma::umin3;
 
-constexpr int BW_NW = 8;             // waves per workgroup: 4 searchers, 4 producers
-constexpr int BW_T = 64 * BW_NW;     // threads
 constexpr int BW_RAWN = 6;           // raw slab ring (slabs b + 1 .. b + 6 at band b)
-constexpr int BW_P0N = 5;            // P0 planes: the band searched + 4 in production
-constexpr int BW_XN = 4;             // XOR-ed slabs: ring of 3 + the mirror of slot 0
 constexpr int BW_OPS = 46;           // producer steps per band: 16 rows in, then 15 x (out, in)
-constexpr int BW_OPS_IT = 12;        // producer steps per iteration (4 iterations per band)
+
+// The rings of a workgroup with PW producer waves: band m is produced over the
+// PW iterations before it is searched (phase t in iteration m - PW + t).
+template <int PW>
+struct BwRings {
+  static constexpr int IT = (BW_OPS + PW - 1) / PW;  // producer steps per iteration
+  static constexpr int P0N = PW + 1;                 // P0 planes: the band searched + PW in production
+  static constexpr int XR = PW + 1;                  // XOR-ed slab ring (slab s in slot s % XR)
+  static constexpr int XN = XR + 1;                  // + the mirror of slot 0
+  static constexpr int E = IT > 16 ? 1 : 0;          // phase 0 also reads slab m + 1
+};
 constexpr int BW_CREC = 48;          // cur row record: 16 zero bytes, the row (c ^ 0x7F), 16 zero bytes
 
 #ifdef ME_STAMPS
@@ -79,7 +89,8 @@ constexpr int BW_CREC = 48;          // cur row record: 16 zero bytes, the row (
 // s_memtime cycles spent in each phase of the band loop, summed over the
 // iterations: [prologue, entries / slab DMA + XOR, fetch, tiles, band end,
 // production, barrier wait, iterations] (tools/bw_stamps.py).
-__device__ unsigned long long g_bwstamps[8 * 8 * 4096];
+constexpr int BW_STW = 16;  // waves per workgroup slot
+__device__ unsigned long long g_bwstamps[BW_STW * 8 * 4096];
 #define BW_T0() unsigned long long bw_t = __builtin_amdgcn_s_memtime()
 #define BW_ACC(k) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); bw_acc[k] += t_ - bw_t; bw_t = t_; } while (0)
 #else
@@ -100,23 +111,36 @@ __device__ __forceinline__ uint32_t ld32(uint32_t a) {
 __device__ __forceinline__ v4i ldv4(uint32_t a) {
   return *reinterpret_cast<lds_cv4i*>((uintptr_t)a);
 }
-// (a << 7) + b in one instruction
-__device__ __forceinline__ uint32_t lshl7_add(uint32_t a, uint32_t b) {
-  uint32_t d;
-  asm("v_lshl_add_u32 %0, %1, 7, %2" : "=v"(d) : "v"(a), "v"(b));
-  return d;
-}
 
 // LDS layout (bytes): XN slabs | RAWN slabs | P0N planes | crec (searchers) | keys
 __host__ __device__ constexpr int bw_slab(int lp) { return 16 * lp; }
-__host__ __device__ inline int bw_lds_bytes(int lp, int pp, int ns) {
-  return (BW_XN + BW_RAWN) * bw_slab(lp) + BW_P0N * 16 * pp * 4 + 4 * 16 * BW_CREC + 4 * ns * 8;
+__host__ __device__ inline int bw_lds_bytes(int lp, int pp, int ns, int nsw, int pw) {
+  return (pw + 2 + BW_RAWN) * bw_slab(lp) + (pw + 1) * 16 * pp * 4 + nsw * 16 * BW_CREC + nsw * ns * 8;
 }
 
-template <int C, int NS, int LP>
-__global__ __launch_bounds__(BW_T) void me_mfma_bw_kernel(SearchArgs p, MfmaGeom g, MfmaJobs jb) {
-  constexpr int WPC = 4 / C;  // row classes per column
+// Waits until at most n of this wave's vector-memory operations are
+// outstanding (s_waitcnt takes an immediate).
+__device__ __forceinline__ void wait_vm(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+  }
+}
+
+// NSW searcher waves + PW producer waves; <= 128 VGPRs (four waves per SIMD:
+// one workgroup of 16 waves, or two of 8, per CU)
+template <int C, int NS, int LP, int NSW, int PW, bool ABL>
+__global__ __launch_bounds__(64 * (NSW + PW), 4) void me_mfma_bw_kernel(SearchArgs p, MfmaGeom g, MfmaJobs jb) {
+  using R = BwRings<PW>;
+  constexpr int BW_P0N = R::P0N, BW_XR = R::XR, BW_XN = R::XN, BW_OPS_IT = R::IT;
+  constexpr int WPC = NSW / C;  // row classes per column
   constexpr int SLAB = bw_slab(LP);
+  // DMA instructions of this wave per slab (1,024 bytes each, dealt round the producers)
   extern __shared__ __align__(16) uint8_t smem[];
   const int PP = g.bw_pp;
   const int P0PLANE = 16 * PP;  // ints
@@ -124,13 +148,14 @@ __global__ __launch_bounds__(BW_T) void me_mfma_bw_kernel(SearchArgs p, MfmaGeom
   uint8_t* raw = xw + BW_XN * SLAB;
   int* p0 = reinterpret_cast<int*>(raw + BW_RAWN * SLAB);
   uint8_t* crec_all = reinterpret_cast<uint8_t*>(p0 + BW_P0N * P0PLANE);
-  unsigned long long* keys = reinterpret_cast<unsigned long long*>(crec_all + 4 * 16 * BW_CREC);
+  unsigned long long* keys = reinterpret_cast<unsigned long long*>(crec_all + NSW * 16 * BW_CREC);
 
   const int tid = (int)threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const bool searcher = wave < 4;
-  const int col = wave % C, cls = (wave & 3) / C;  // searchers
-  const int pw = wave & 3, ptid = tid & 255;       // producers: index, thread within the role
+  const bool searcher = wave < NSW;
+  const int col = wave % C, cls = wave / C;                // searchers
+  const int pw = wave - NSW;                               // producers: index
+  const int nps = pw >= 0 && pw * 1024 < SLAB ? (SLAB - pw * 1024 + PW * 1024 - 1) / (PW * 1024) : 0;
   const int n = lane & 15, h = lane >> 4;
   const int S = p.range, W = p.width, H = p.height;
   int lin = mfma::xcd_banded_index();
@@ -162,7 +187,7 @@ __global__ __launch_bounds__(BW_T) void me_mfma_bw_kernel(SearchArgs p, MfmaGeom
   auto dma_slab = [&](int s) {
     uint8_t* dst = raw + (s % BW_RAWN) * SLAB;
     const int rowb = 16 * s - p.ref_row0;
-    for (int s0 = pw * 1024; s0 < SLAB; s0 += 4 * 1024) {
+    for (int s0 = pw * 1024; s0 < SLAB; s0 += PW * 1024) {
       const int d = s0 + 16 * lane;
       if (d < SLAB) {
         const int rho = d / LP, k = d - rho * LP;
@@ -172,20 +197,6 @@ __global__ __launch_bounds__(BW_T) void me_mfma_bw_kernel(SearchArgs p, MfmaGeom
       }
     }
   };
-  // slab s XOR-ed (r ^ 0x80 = r - 128 as i8, the B operand) into ring slot s % 3
-  // and, for slot 0, its mirror after slot 2: band b's rows 16 b .. 16 b + 30
-  // are then contiguous from slot b % 3
-  auto xor_slab = [&](int s) {
-    const u32x4* src = reinterpret_cast<const u32x4*>(raw + (s % BW_RAWN) * SLAB);
-    const int slot = s % 3;
-    u32x4* dst = reinterpret_cast<u32x4*>(xw + slot * SLAB);
-    u32x4* mir = reinterpret_cast<u32x4*>(xw + 3 * SLAB);
-    for (int t = ptid; t < SLAB / 16; t += 256) {
-      const u32x4 v = src[t] ^ 0x80808080u;
-      dst[t] = v;
-      if (slot == 0) mir[t] = v;
-    }
-  };
   // V(row) = sum of 16 window rows of H, H(row, x) = sum over the 4 bytes at
   // x of (r - 127)^2 (u = r ^ 0x7F = 127 - r as an i8: one v_dot4 per 4
   // bytes).  Lane (row R, l) owns the 4 positions of group pg = 13 R + l: the
@@ -193,6 +204,7 @@ __global__ __launch_bounds__(BW_T) void me_mfma_bw_kernel(SearchArgs p, MfmaGeom
   // in its own row (l < 13 outputs).
   const int pg = 13 * (lane >> 4) + (lane & 15);
   const bool pout = (lane & 15) < 13 && 4 * pg < npos;
+  const bool pxor = (lane & 15) < 13 && 4 * pg < LP;  // writes the XOR-ed window bytes 4 pg .. 4 pg + 3
   v4i V = {0, 0, 0, 0};
   auto h_acc = [&](uint32_t w0, uint32_t w1, v4i acc) {  // acc + H of the bytes (w0, w1)
     const uint32_t u0 = w0 ^ 0x7F7F7F7Fu, u1 = w1 ^ 0x7F7F7F7Fu;
@@ -215,32 +227,54 @@ __global__ __launch_bounds__(BW_T) void me_mfma_bw_kernel(SearchArgs p, MfmaGeom
       v4i o;
 #pragma unroll
       for (int r = 0; r < 4; r++) o[r] = (int)lshl6_add((uint32_t)Q[r], (1u << 29) + 64u + (uint32_t)r);
-      *reinterpret_cast<v4i*>(p0 + (m % BW_P0N) * P0PLANE + j * PP + 4 * pg) = o;
+      // the lane's base recomputed per row (opaque): hoisted, the 16 row
+      // addresses pinned 16 VGPRs and spilled
+      typedef __attribute__((address_space(3))) v4i lds_v4i;
+      const uint32_t pa = (uint32_t)opaque((int)lds_addr(p0 + 4 * pg)) +
+                          4u * (uint32_t)((m % BW_P0N) * P0PLANE + j * PP);
+      *reinterpret_cast<lds_v4i*>((uintptr_t)pa) = o;
     }
   };
-  // steps [o0, o1) of band m (at most BW_OPS_IT): 0..15 add rows 0..15 (row
-  // 0 out after 15), then for j = 1..15: remove row j - 1, add row j + 15,
-  // row j out.  The window rows of all the steps are read first: one LDS
-  // latency per call.
-  auto produce = [&](int m, int o0, int o1) {
-    uint32_t w0[BW_OPS_IT], w1[BW_OPS_IT];
+  // Steps [O0, O1) of band m (compile-time, at most 12): 0..15 add rows
+  // 0..15 (row 0 out after 15), then for j = 1..15: remove row j - 1, add
+  // row j + 15, row j out.  Straight-line code; the window rows of all the
+  // steps are read first (one LDS latency).  Steps 0..15 read slab m's rows
+  // once, so they also store them XOR-ed with 0x80 (r - 128 as an i8: the
+  // MFMA B operand) into ring slot m % XR, and slot 0 into the mirror after
+  // slot XR - 1: band b's rows 16 b .. 16 b + 30 are then contiguous from
+  // slot b % XR.  Band m is produced in iterations m - PW .. m - 1 of the
+  // walk; the slot's previous slab (m - XR) was last read by band m - XR.
+  // Band m > blast (the last slab, bend) runs the phases with steps below 16
+  // for the XOR only (no P0 rows).
+  auto steps = [&](auto c0, auto c1, int m) __attribute__((always_inline)) {
+    constexpr int O0 = decltype(c0)::value;
+    constexpr int O1 = decltype(c1)::value;
+    const bool outp = m <= blast;
+    const uint32_t xa = lds_addr(xw + (m % BW_XR) * SLAB) + 4u * (uint32_t)pg;
+    const bool mirror = m % BW_XR == 0;
+    uint32_t w0[12], w1[12];
 #pragma unroll
-    for (int k = 0; k < BW_OPS_IT; k++) {
-      const int o = min(o0 + k, o1 - 1), q = o - 16;
+    for (int o = O0; o < O1; o++) {
+      const int q = o - 16;
       const int rho = o < 16 ? o : (q & 1) ? (q >> 1) + 16 : (q >> 1);
       const uint32_t a = lds_addr(raw + ((m + (rho >> 4)) % BW_RAWN) * SLAB + (rho & 15) * LP) +
                          4u * (uint32_t)pg;
-      w0[k] = ld32(a);
-      w1[k] = ld32(a + 4);
+      w0[o - O0] = ld32(a);
+      w1[o - O0] = ld32(a + 4);
     }
 #pragma unroll
-    for (int k = 0; k < BW_OPS_IT; k++) {
-      const int o = o0 + k;
-      if (o >= o1) break;
+    for (int o = O0; o < O1; o++) {
+      const int k = o - O0;
       if (o < 16) {
+        if (pxor) {
+          typedef __attribute__((address_space(3))) uint32_t lds_u32;
+          const uint32_t xv = w0[k] ^ 0x80808080u;
+          *reinterpret_cast<lds_u32*>((uintptr_t)(xa + (uint32_t)(o * LP))) = xv;
+          if (mirror) *reinterpret_cast<lds_u32*>((uintptr_t)(xa + (uint32_t)(BW_XR * SLAB + o * LP))) = xv;
+        }
         const v4i z = {0, 0, 0, 0};
         V = h_acc(w0[k], w1[k], o == 0 ? z : V);
-        if (o == 15) out_row(m, 0);
+        if (o == 15 && outp) out_row(m, 0);
       } else {
         const int q = o - 16, j = (q >> 1) + 1;
         if ((q & 1) == 0) {
@@ -248,11 +282,40 @@ __global__ __launch_bounds__(BW_T) void me_mfma_bw_kernel(SearchArgs p, MfmaGeom
           V -= h_acc(w0[k], w1[k], z);
         } else {
           V = h_acc(w0[k], w1[k], V);
-          out_row(m, j);
+          if (outp) out_row(m, j);
         }
       }
     }
   };
+  // phase T of band m: steps [IT T, min(IT T + IT, 46)), in chunks of 12
+  auto produce = [&](auto tc, int m) __attribute__((always_inline)) {
+    constexpr int T = decltype(tc)::value;
+    constexpr int O0 = BW_OPS_IT * T;
+    constexpr int O1 = O0 + BW_OPS_IT < BW_OPS ? O0 + BW_OPS_IT : BW_OPS;
+    constexpr int O2 = O0 + 12 < O1 ? O0 + 12 : O1;
+    steps(std::integral_constant<int, O0>{}, std::integral_constant<int, O2>{}, m);
+    if constexpr (O2 < O1) {
+      constexpr int O3 = O2 + 12 < O1 ? O2 + 12 : O1;
+      steps(std::integral_constant<int, O2>{}, std::integral_constant<int, O3>{}, m);
+      static_assert(O3 == O1, "at most two chunks per phase");
+    }
+  };
+  auto produce_phase = [&](int t, int m) __attribute__((always_inline)) {
+    if constexpr (PW == 2) {
+      if (t == 0) produce(std::integral_constant<int, 0>{}, m);
+      else produce(std::integral_constant<int, 1>{}, m);
+    } else {
+      switch (t) {
+        case 0: produce(std::integral_constant<int, 0>{}, m); break;
+        case 1: produce(std::integral_constant<int, 1>{}, m); break;
+        case 2: produce(std::integral_constant<int, 2>{}, m); break;
+        default: produce(std::integral_constant<int, 3>{}, m); break;
+      }
+    }
+  };
+  // phases of band m == bend (the XOR of the last slab only): those with
+  // steps below 16
+  constexpr int XPH = (15 / BW_OPS_IT) + 1;
 
   // ================================ searchers
   // block rows in flight: a ring of NS slots (this searcher's class)
@@ -272,7 +335,7 @@ __global__ __launch_bounds__(BW_T) void me_mfma_bw_kernel(SearchArgs p, MfmaGeom
   const int bx = 16 * (bc0 + col);
   const int xlo = max(bx - S, 0), xhi = min(bx + S, W - 16);
   const int i0c = xlo >> 4, i1c = xhi >> 4;
-  uint8_t* crec = crec_all + (wave & 3) * 16 * BW_CREC;
+  uint8_t* crec = crec_all + wave * 16 * BW_CREC;
   const uint8_t* cur_lane = p.cur + (ptrdiff_t)(lane - p.cur_row0) * p.stride + 16 * (bc0 + col);
 
   // The first row entering at band b (this column and class) is prefetched
@@ -316,20 +379,23 @@ __global__ __launch_bounds__(BW_T) void me_mfma_bw_kernel(SearchArgs p, MfmaGeom
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     const int o = 16 + 16 * (h & 1) - n, sh = o & 3;
     const uint32_t lb = lds_addr(crec) + (uint32_t)((h >> 1) * BW_CREC + (o & ~3));
-    uint32_t d[8][5];  // every record read first: one LDS latency
-#pragma unroll
-    for (int q = 0; q < 8; q++)
-#pragma unroll
-      for (int e = 0; e < 5; e++) d[q][e] = ld32(lb + (uint32_t)(2 * q * BW_CREC + 4 * e));
 #pragma unroll
     for (int s = 0; s < NS; s++) {
       if (s != slot) continue;
 #pragma unroll
-      for (int q = 0; q < 8; q++) {
-        v4i f;
+      for (int q0 = 0; q0 < 8; q0 += 4) {  // half the records read at a time: one LDS latency each
+        uint32_t d[4][5];
 #pragma unroll
-        for (int e = 0; e < 4; e++) f[e] = (int)__builtin_amdgcn_alignbyte(d[q][e + 1], d[q][e], sh);
-        A[s][q] = f;
+        for (int q = 0; q < 4; q++)
+#pragma unroll
+          for (int e = 0; e < 5; e++) d[q][e] = ld32(lb + (uint32_t)(2 * (q0 + q) * BW_CREC + 4 * e));
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          v4i f;
+#pragma unroll
+          for (int e = 0; e < 4; e++) f[e] = (int)__builtin_amdgcn_alignbyte(d[q][e + 1], d[q][e], sh);
+          A[s][q0 + q] = f;
+        }
       }
       srow[s] = br;
       cc[s] = ccv;
@@ -342,7 +408,7 @@ __global__ __launch_bounds__(BW_T) void me_mfma_bw_kernel(SearchArgs p, MfmaGeom
   auto emit = [&](int s) {
     const int br = srow[s];
     const uint32_t kb = bk[s], hk = kb >> 6;
-    unsigned long long* kp = keys + (wave & 3) * NS + s;
+    unsigned long long* kp = keys + wave * NS + s;
     if (hk < (1u << 25)) {
       const uint32_t cost = hk - 1u - (1u << 23) + (uint32_t)cc[s];
       const int idx = (int)(kb & 63u);
@@ -365,113 +431,159 @@ __global__ __launch_bounds__(BW_T) void me_mfma_bw_kernel(SearchArgs p, MfmaGeom
 #ifdef ME_STAMPS
   unsigned long long bw_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
+  if (ABL && (g.bw_abl & 16)) {
+    if (!searcher) __builtin_amdgcn_s_setprio(1);
+  } else if (ABL && (g.bw_abl & 32)) {
+    if (searcher) __builtin_amdgcn_s_setprio(1);
+  }
   BW_T0();
   // ---- prologue: the first slabs, the keys, the first two XOR-ed slabs, the
   // production steps the schedule puts before iteration 0, the first rows
   if (!searcher)
     for (int s = bfirst; s < bfirst + BW_RAWN && s <= bend; s++) dma_slab(s);
-  if (tid < 4 * NS) keys[tid] = ~0ull;
+  if (tid < NSW * NS) keys[tid] = ~0ull;
   if (searcher) fetch(bfirst);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // The DMA ring runs ahead: production in iteration b reads raw slabs up to
+  // b + PW + E, so a producer waits only for its DMAs of the slabs up to the
+  // ones it reads next (nps DMA instructions per slab and wave, in order),
+  // not for the ones just issued.  The prologue's production reads slabs up
+  // to bfirst + PW - 1 + E.
+  const int dlast = min(bfirst + BW_RAWN - 1, bend);  // the prologue's DMAs: slabs bfirst .. dlast
+  if (!searcher) wait_vm(nps * max(0, dlast - (bfirst + PW - 1 + R::E)));
   __syncthreads();
   if (!searcher) {
-    xor_slab(bfirst);
-    if (bfirst + 1 <= bend) xor_slab(bfirst + 1);
-    if (bfirst + pw <= blast && !(g.bw_abl & 1)) {
-      const int oend = min(BW_OPS_IT * (4 - pw), BW_OPS);
-      for (int o = 0; o < oend; o += BW_OPS_IT) produce(bfirst + pw, o, min(o + BW_OPS_IT, oend));
+    if (bfirst + pw <= bend && !(ABL && (g.bw_abl & 1))) {
+      const int tend = bfirst + pw <= blast ? PW - pw : min(PW - pw, XPH);
+      for (int t = 0; t < tend; t++) produce_phase(t, bfirst + pw);
     }
+    wait_vm(nps * max(0, dlast - (bfirst + PW + R::E)));  // iteration 0's slabs
+  } else if (hascol && !(ABL && (g.bw_abl & 4))) {
+    for (int br = pe0; br < pe1; br += WPC)
+      enter(br, br == pe0 ? pf0 : *reinterpret_cast<const u32x4*>(cur_lane + (ptrdiff_t)(16 * br) * p.stride));
   }
   __syncthreads();
   BW_ACC(0);
 
   const int nit = blast - bfirst + 1;
+  // Two loops, one per role, each with one barrier per band: the searchers'
+  // ring (A fragments, bests) is not live in the producers' loop.
+  if (!searcher) {
+    for (int it = 0; it < nit; it++) {
+      const int b = bfirst + it;
+      if (b + BW_RAWN <= bend) dma_slab(b + BW_RAWN);
+      BW_ACC(1);
+      // band b + 1 + d, d = (pw - it - 1) mod PW, its phase PW - 1 - d
+      const int d = ((pw - it - 1) % PW + PW) % PW;
+      const int m = b + 1 + d, t = PW - 1 - d;
+      if ((m <= blast || (m == bend && t < XPH)) && !(ABL && (g.bw_abl & 1))) produce_phase(t, m);
+      BW_ACC(5);
+      // the slabs iteration b + 1 reads (up to b + 1 + PW + E) landed; the
+      // later ones may still be in flight
+      wait_vm(nps * max(0, min(b + BW_RAWN, bend) - (b + 1 + PW + R::E)));
+      __syncthreads();
+      BW_ACC(6);
+    }
+  } else {
   for (int it = 0; it < nit; it++) {
     const int b = bfirst + it;
-    if (!searcher) {
-      if (b + BW_RAWN <= bend) dma_slab(b + BW_RAWN);
-      if (b + 2 <= bend && !(g.bw_abl & 8)) xor_slab(b + 2);
-      BW_ACC(1);
-      // band first + m', m' = it + 1 + ((pw - it - 1) & 3), its steps of this iteration
-      const int d = (pw - it - 1) & 3;
-      const int m = b + 1 + d, t = 3 - d;
-      if (m <= blast && !(g.bw_abl & 1)) produce(m, BW_OPS_IT * t, min(BW_OPS_IT * (t + 1), BW_OPS));
-      BW_ACC(5);
-    } else if (hascol) {
-      if (!(g.bw_abl & 4))
-        for (int br = pe0; br < pe1; br += WPC)
-          enter(br, br == pe0 ? pf0 : *reinterpret_cast<const u32x4*>(cur_lane + (ptrdiff_t)(16 * br) * p.stride));
-      BW_ACC(1);
-      fetch(b + 1);
+    if (hascol) {
+      // the rows entering at band b + 1: their cur rows load during this
+      // band's tiles, they enter after its end (a wave that finishes its
+      // tiles early does its entries while the SIMD's other waves still run
+      // MFMAs, instead of every wave at the start of the band)
+      if (b + 1 <= blast) fetch(b + 1);
       BW_ACC(2);
-      if (!(g.bw_abl & 2)) {
-        // y validity of the band's rows per row in flight: bit 31 on the keys
-        // of rows outside the row's range (partial bands only)
-        uint32_t ym[NS];
-        bool act[NS], ypart[NS];
+      if (!(ABL && (g.bw_abl & 2))) {
+        // y validity per row in flight: a lane forms the keys of one candidate
+        // row (y = 16 b + n) only, so a row outside the block's range (the
+        // range's partial bands) drops the lane's band best at the band end
+        bool act[NS], yok[NS];
 #pragma unroll
         for (int s = 0; s < NS; s++) {
           act[s] = srow[s] >= 0;
           const int ylo = max(16 * srow[s] - S, 0), yhi = min(16 * srow[s] + S, H - 16);
           const int y = 16 * b + n;
-          ym[s] = (y < ylo || y > yhi) ? 0x80000000u : 0u;
-          ypart[s] = 16 * b < ylo || 16 * b + 15 > yhi;
+          yok[s] = y >= ylo && y <= yhi;
         }
-        const uint32_t xb = lds_addr(xw + (b % 3) * SLAB) +
-                            (uint32_t)((n + (h >> 1)) * LP + 16 * (h & 1) - 16 * tc0);
-        const uint32_t pb = lds_addr(p0 + (b % BW_P0N) * P0PLANE) + (uint32_t)((n * PP + 4 * h - 16 * tc0) * 4);
-        // fragments through a ring of 4 registers, two fragments ahead
-        // (fragment q of tile i: window row n + 2 q + (h >> 1), column 16 i + 16 (h & 1))
-        v4i f[4];
-        {
-          const uint32_t l0 = (uint32_t)opaque((int)(xb + (uint32_t)(16 * i0c)));
-          f[0] = ldv4(l0);
-          f[1] = ldv4(l0 + (uint32_t)(2 * LP));
-        }
-        const v4i zero4 = {0, 0, 0, 0};
+        // the tiles of the band for the active slots M (compile-time: no MFMA
+        // for a free slot)
+        auto tiles = [&](auto mc) __attribute__((always_inline)) {
+          constexpr int M = decltype(mc)::value;
+          const uint32_t xb = lds_addr(xw + (b % BW_XR) * SLAB) +
+                              (uint32_t)((n + (h >> 1)) * LP + 16 * (h & 1) - 16 * tc0);
+          const uint32_t pb = lds_addr(p0 + (b % BW_P0N) * P0PLANE) + (uint32_t)((n * PP + 4 * h - 16 * tc0) * 4);
+          // fragments through a ring of 4 registers, three fragments ahead
+          // (fragment q of tile i: window row n + 2 q + (h >> 1), column 16 i + 16 (h & 1))
+          v4i f[4];
+          {
+            const uint32_t l0 = (uint32_t)opaque((int)(xb + (uint32_t)(16 * i0c)));
+            f[0] = ldv4(l0);
+            f[1] = ldv4(l0 + (uint32_t)(2 * LP));
+            f[2] = ldv4(l0 + (uint32_t)(4 * LP));
+          }
+          const v4i zero4 = {0, 0, 0, 0};
+          // tile i, prefetching tile inx; E: the column's first or last tile,
+          // where the block's x range may end (bit 31 on the position term)
+          auto tile = [&](auto ec, int i, int inx) __attribute__((always_inline)) {
+            constexpr bool E = decltype(ec)::value;
+            const uint32_t lcur = (uint32_t)opaque((int)(xb + (uint32_t)(16 * i)));
+            const uint32_t lnext = (uint32_t)opaque((int)(xb + (uint32_t)(16 * inx)));
+            const v4i pv = ldv4(pb + (uint32_t)(64 * i));
+            v4i acc[NS];
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+              const int qn = q + 3;
+              if (!(ABL && (g.bw_abl & 128)))
+                f[qn & 3] = ldv4(qn < 8 ? lcur + (uint32_t)(2 * qn * LP) : lnext + (uint32_t)(2 * (qn - 8) * LP));
+#pragma unroll
+              for (int s = 0; s < NS; s++)
+                if ((M >> s) & 1) acc[s] = MFMA16(A[s][q], f[q & 3], q == 0 ? zero4 : acc[s], 0, 0, 0);
+            }
+            const uint32_t rel4 = 4u * (uint32_t)(i - i0c);
+            uint32_t P[4];
+#pragma unroll
+            for (int r = 0; r < 4; r++) P[r] = (uint32_t)pv[r] + rel4;
+            if constexpr (E) {
+#pragma unroll
+              for (int r = 0; r < 4; r++) {
+                const int x = 16 * i + 4 * h + r;
+                P[r] |= (x < xlo || x > xhi) ? 0x80000000u : 0u;
+              }
+            }
+            if (ABL && (g.bw_abl & 64)) {  // timing only: no key epilogue
+#pragma unroll
+              for (int s = 0; s < NS; s++)
+                if ((M >> s) & 1) bcur[s] ^= (uint32_t)acc[s][0];
+              return;
+            }
+#pragma unroll
+            for (int s = 0; s < NS; s++) {
+              if (!((M >> s) & 1)) continue;
+              uint32_t k[4];
+#pragma unroll
+              // plain C, not inline asm: the compiler must see this read of the
+              // MFMA result to insert the wait states the hardware does not
+              // interlock (an asm read right after the MFMA read stale values)
+              for (int r = 0; r < 4; r++) k[r] = ((uint32_t)acc[s][r] << 7) + P[r];
+              bcur[s] = umin3(umin3(bcur[s], k[0], k[1]), k[2], k[3]);
+            }
+          };
+          tile(std::true_type{}, i0c, min(i0c + 1, i1c));
 #pragma unroll 1
-        for (int i = i0c; i <= i1c; i++) {
-          const int inx = i < i1c ? i + 1 : i;  // the last tile prefetches itself (unused)
-          const uint32_t lcur = (uint32_t)opaque((int)(xb + (uint32_t)(16 * i)));
-          const uint32_t lnext = (uint32_t)opaque((int)(xb + (uint32_t)(16 * inx)));
-          const v4i pv = ldv4(pb + (uint32_t)(64 * i));
-          v4i acc[NS];
+          for (int i = i0c + 1; i < i1c; i++) tile(std::false_type{}, i, i + 1);
+          if (i1c > i0c) tile(std::true_type{}, i1c, i1c);
+        };
+        int am = 0;
 #pragma unroll
-          for (int q = 0; q < 8; q++) {
-            const int qn = q + 2;
-            f[qn & 3] = ldv4(qn < 8 ? lcur + (uint32_t)(2 * qn * LP) : lnext + (uint32_t)(2 * (qn - 8) * LP));
-#pragma unroll
-            for (int s = 0; s < NS; s++) acc[s] = MFMA16(A[s][q], f[q & 3], q == 0 ? zero4 : acc[s], 0, 0, 0);
-          }
-          const uint32_t rel4 = 4u * (uint32_t)(i - i0c);
-          uint32_t P[4];
-#pragma unroll
-          for (int r = 0; r < 4; r++) P[r] = (uint32_t)pv[r] + rel4;
-          // x validity on the column's first / last tile: bit 31
-          const bool edge = i == i0c || i == i1c;
-          uint32_t mk[4] = {0u, 0u, 0u, 0u};
-          if (edge) {
-#pragma unroll
-            for (int r = 0; r < 4; r++) {
-              const int x = 16 * i + 4 * h + r;
-              mk[r] = (x < xlo || x > xhi) ? 0x80000000u : 0u;
-            }
-          }
-#pragma unroll
-          for (int s = 0; s < NS; s++) {
-            uint32_t k[4];
-#pragma unroll
-            for (int r = 0; r < 4; r++) k[r] = lshl7_add((uint32_t)acc[s][r], P[r]);
-            if (edge) {
-#pragma unroll
-              for (int r = 0; r < 4; r++) k[r] |= mk[r];
-            }
-            if (ypart[s]) {
-#pragma unroll
-              for (int r = 0; r < 4; r++) k[r] |= ym[s];
-            }
-            bcur[s] = umin3(umin3(bcur[s], k[0], k[1]), k[2], k[3]);
-          }
+        for (int s = 0; s < NS; s++) am |= act[s] ? 1 << s : 0;
+        am = __builtin_amdgcn_readfirstlane(am);
+        if (ABL && (g.bw_abl & 256)) am &= 1;  // timing only: slot 0's MFMAs only
+        if constexpr (NS == 2) {
+          if (am == 3) tiles(std::integral_constant<int, 3>{});
+          else if (am == 1) tiles(std::integral_constant<int, 1>{});
+          else if (am == 2) tiles(std::integral_constant<int, 2>{});
+        } else {
+          if (am) tiles(std::integral_constant<int, (1 << NS) - 1>{});
         }
         BW_ACC(3);
         // band end: the lane's best of the band into the row's best (an earlier
@@ -479,7 +591,7 @@ __global__ __launch_bounds__(BW_T) void me_mfma_bw_kernel(SearchArgs p, MfmaGeom
 #pragma unroll
         for (int s = 0; s < NS; s++) {
           if (!act[s]) continue;
-          if ((bcur[s] >> 6) < (bk[s] >> 6)) {
+          if (yok[s] && (bcur[s] >> 6) < (bk[s] >> 6)) {
             bk[s] = bcur[s];
             bb[s] = b;
           }
@@ -491,15 +603,19 @@ __global__ __launch_bounds__(BW_T) void me_mfma_bw_kernel(SearchArgs p, MfmaGeom
         }
         BW_ACC(4);
       }
+      if (b + 1 <= blast && !(ABL && (g.bw_abl & 4)))
+        for (int br = pe0; br < pe1; br += WPC)
+          enter(br, br == pe0 ? pf0 : *reinterpret_cast<const u32x4*>(cur_lane + (ptrdiff_t)(16 * br) * p.stride));
+      BW_ACC(1);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // DMA'd slab and fetched cur rows landed
     __syncthreads();
     BW_ACC(6);
+  }
   }
 #ifdef ME_STAMPS
   if (lane == 0 && blockIdx.x < 4096) {
     bw_acc[7] = (unsigned long long)nit;
-    for (int k = 0; k < 8; k++) g_bwstamps[(blockIdx.x * 8 + wave) * 8 + k] = bw_acc[k];
+    for (int k = 0; k < 8; k++) g_bwstamps[(blockIdx.x * BW_STW + wave) * 8 + k] = bw_acc[k];
   }
 #endif
 }
@@ -532,26 +648,42 @@ bool plan_bw(const SearchArgs& p, MfmaGeom* g, int jobs) {
   if (p.stride % 16 || (uintptr_t)p.cur % 16) return false;  // 16-byte cur row loads
   const int rows = g->nrows - (g->hb_row >= 0 ? 1 : 0);       // full-height rows
   if (rows < 1 || g->nbx < 1) return false;
-  // Three ring slots per searcher (A fragments of 3 rows: 96 VGPRs): the
-  // 2 ceil(S/16) + 1 rows in flight of a column split over 4 / C searchers.
-  // S <= 16: 4 columns, one searcher each (3 rows); S <= 32: 2 columns, two
-  // searchers each (5 rows); S <= 64: 1 column, four searchers (9 rows).
-  const int C = S <= 16 ? 4 : S <= 32 ? 2 : 1;
-  const int ns = 3;
+  // Two ring slots per searcher wave (A fragments of 2 rows: 64 VGPRs): the
+  // 2 ceil(S/16) + 1 rows in flight of a column split over nsw / C
+  // searchers, the widest strip whose column fits its rows.  Two shapes, both
+  // four waves per SIMD at <= 128 VGPRs:
+  //   - one workgroup of 12 searchers + 4 producers (the default):
+  //     S <= 16: 6 columns; S <= 32: 4; S <= 48: 3; S <= 64: 2;
+  //   - two workgroups per CU of 6 searchers + 2 producers (ME_BW_WG=2,
+  //     tuning build): S <= 16: 3 columns; S <= 32: 2; S <= 64: 1.  Measured
+  //     slower at 1080p (32.4 against 27.9 us per frame of a 16-frame batch,
+  //     equal at 4K: profiles/r05w_ssd_ab.jsonl).
+  const bool big = tuning().bw_wg != 2;
+  const int nsw = big ? 12 : 6, npw = big ? 4 : 2, ns = 2, wgs_cu = big ? 1 : 2;
+  const int inflight = 2 * ((S + 15) / 16) + 1;
+  int C = 0;
+  for (int c : {6, 4, 3, 2, 1})
+    if (nsw % c == 0 && (nsw / c) * ns >= inflight) {
+      C = c;
+      break;
+    }
+  if (C == 0) return false;
   const int npos_max = 16 * ((16 * (C - 1) + 2 * S) / 16 + 2);
-  const int lp = C == 1 ? 224 : 160;
+  const int lp = npos_max + 16 <= 160 ? 160 : 224;
   if (npos_max + 16 > lp || npos_max / 4 > 52) return false;  // 4 lane rows x 13 output groups
   const int pp = pitch_at_least(npos_max, 8, 16);
-  g->bw_wpc = 4 / C;
+  g->bw_wpc = nsw / C;
   g->bw_ns = ns;
+  g->bw_nsw = nsw;
+  g->bw_pw = npw;
   g->bw_cols = C;
   g->bw_lp = lp;
   g->bw_pp = pp;
   g->bw_strips = (g->nbx + C - 1) / C;
-  // Segment rows: a workgroup per CU; rounds of workgroups x (segment bands +
-  // the 2 ceil(S/16) extra bands + ~2 bands of prologue), the smallest
+  // Segment rows: rounds of resident workgroups x (segment bands + the
+  // 2 ceil(S/16) extra bands + ~2 bands of prologue), the smallest
   int best_t = 1 << 30, best_l = rows;
-  const int cus = bw_cu_count(), extra = 2 * ((S + 15) / 16) + 2;
+  const int cus = bw_cu_count() * wgs_cu, extra = 2 * ((S + 15) / 16) + 2;
   const long per = (long)std::max(jobs, 1) * g->bw_strips;
   for (int L = rows; L >= 4; L--) {
     const long segs = (rows + L - 1) / L;
@@ -567,8 +699,8 @@ bool plan_bw(const SearchArgs& p, MfmaGeom* g, int jobs) {
   g->bw_seg_rows = best_l;
   g->bw_abl = tuning().bw_abl;
   g->bw_segs = (rows + best_l - 1) / best_l;
-  g->lds = bw_lds_bytes(lp, pp, ns);
-  if (g->lds > 160 * 1024) return false;
+  g->lds = bw_lds_bytes(lp, pp, ns, nsw, npw);
+  if (g->lds > 160 * 1024 / wgs_cu) return false;
   g->bw = 1;
   return true;
 }
@@ -578,16 +710,25 @@ hipError_t launch_bw(const SearchArgs& p, const MfmaGeom& g0, const MfmaJobs& jb
   g.nrows = g0.nrows - (g0.hb_row >= 0 ? 1 : 0);  // full-height rows: the kernel's
   MfmaJobs jb = jb0;
   jb.wgs = g.bw_strips * g.bw_segs;
-  const dim3 grid((unsigned)(jb.n * jb.wgs)), blk(BW_T);
+  const dim3 grid((unsigned)(jb.n * jb.wgs)), blk(64 * (g.bw_nsw + g.bw_pw));
   hipError_t e;
-#define ME_BW_CASE(C, NS, LP)                                                            \
-  if (g.bw_cols == C && g.bw_ns == NS && g.bw_lp == LP) {                                \
-    e = lds_attr((const void*)me_mfma_bw_kernel<C, NS, LP>, g.lds);                      \
-    if (e != hipSuccess) return e;                                                       \
-    hipLaunchKernelGGL((me_mfma_bw_kernel<C, NS, LP>), grid, blk, g.lds, stream, p, g, jb); \
-    return hipGetLastError();                                                            \
+  // ablation instances (tuning build only: ME_BW_ABL) are separate kernels
+#define ME_BW_CASE(C, NS, LP, NSW, PW)                                                          \
+  if (g.bw_cols == C && g.bw_ns == NS && g.bw_lp == LP && g.bw_nsw == NSW && g.bw_pw == PW) {   \
+    const void* k = g.bw_abl ? (const void*)me_mfma_bw_kernel<C, NS, LP, NSW, PW, true>         \
+                             : (const void*)me_mfma_bw_kernel<C, NS, LP, NSW, PW, false>;       \
+    e = lds_attr(k, g.lds);                                                                     \
+    if (e != hipSuccess) return e;                                                              \
+    if (g.bw_abl)                                                                               \
+      hipLaunchKernelGGL((me_mfma_bw_kernel<C, NS, LP, NSW, PW, true>), grid, blk, g.lds, stream, p, g, jb); \
+    else                                                                                        \
+      hipLaunchKernelGGL((me_mfma_bw_kernel<C, NS, LP, NSW, PW, false>), grid, blk, g.lds, stream, p, g, jb); \
+    return hipGetLastError();                                                                   \
   }
-  ME_BW_CASE(4, 3, 160) ME_BW_CASE(2, 3, 160) ME_BW_CASE(1, 3, 224)
+  ME_BW_CASE(3, 2, 160, 6, 2) ME_BW_CASE(2, 2, 160, 6, 2) ME_BW_CASE(1, 2, 160, 6, 2)
+  ME_BW_CASE(1, 2, 224, 6, 2)
+  ME_BW_CASE(6, 2, 160, 12, 4) ME_BW_CASE(4, 2, 160, 12, 4) ME_BW_CASE(3, 2, 160, 12, 4)
+  ME_BW_CASE(3, 2, 224, 12, 4) ME_BW_CASE(2, 2, 160, 12, 4) ME_BW_CASE(2, 2, 224, 12, 4)
 #undef ME_BW_CASE
   return hipErrorInvalidValue;
 }
@@ -596,7 +737,7 @@ hipError_t launch_bw(const SearchArgs& p, const MfmaGeom& g0, const MfmaJobs& jb
 
 #ifdef ME_STAMPS
 extern "C" int me_debug_bw_stamps(unsigned long long* out, int n_words) {
-  if (n_words > 8 * 8 * 4096) n_words = 8 * 8 * 4096;
+  if (n_words > me::BW_STW * 8 * 4096) n_words = me::BW_STW * 8 * 4096;
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(me::g_bwstamps), (size_t)n_words * 8, 0,
                                   hipMemcpyDeviceToHost);
 }

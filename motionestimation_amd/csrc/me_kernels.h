@@ -174,7 +174,8 @@ struct MfmaGeom {
   // forming each 16-row band's S2 once in LDS for every block row in flight.
   int bw;                // 1: this plan runs on it (full-height rows [row0, row0 + nrows))
   int bw_wpc, bw_ns;     // waves per block column (row classes), ring slots per wave
-  int bw_cols;           // block columns per strip (8 / bw_wpc)
+  int bw_nsw, bw_pw;     // searcher and producer waves per workgroup
+  int bw_cols;           // block columns per strip (bw_nsw / bw_wpc)
   int bw_strips;         // strips per job
   int bw_seg_rows;       // block rows per workgroup
   int bw_segs;           // segments per job
@@ -203,6 +204,10 @@ size_t merge_tiles_needed(const SearchArgs& p);
 bool mfma_disabled();
 
 hipError_t launch_search(const SearchArgs& p, hipStream_t stream, int* used_fast);
+// Records the kernel family of a search being launched (ME_SEARCH_PATH_*,
+// me_last_search_path).
+void note_path(int path);
+int last_path();
 // Raise fn's dynamic-LDS limit to lds (> 64 KB) on the current device, once
 // per (kernel, device, larger size): process-wide cache, thread-safe.
 hipError_t lds_attr(const void* fn, int lds);

@@ -33,6 +33,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <atomic>
 #include <mutex>
 #include <type_traits>
 #include <vector>
@@ -2016,6 +2017,7 @@ static bool launch_item_jobs(const SearchArgs& base, const SearchJob* jobs, int 
 }
 
 static hipError_t launch_valu(const SearchArgs& p, hipStream_t stream, int* used_fast) {
+  note_path(1);
   if (p.block_row_end <= p.block_row_begin) return hipSuccess;
   const SearchJob J{p.ref, p.ref_row0, p.cur, p.cur_row0, p.block_row_begin, p.block_row_end, p.mv, p.cost};
   hipError_t e;
@@ -2026,16 +2028,26 @@ static hipError_t launch_valu(const SearchArgs& p, hipStream_t stream, int* used
   return launch_items(p, stream, used_fast);
 }
 
+static std::atomic<int> g_last_path{0};
+void note_path(int path) { g_last_path.store(path, std::memory_order_relaxed); }
+int last_path() { return g_last_path.load(std::memory_order_relaxed); }
+
 hipError_t launch_jobs(const SearchArgs& base, const SearchJob* jobs, int n, hipStream_t stream) {
   hipError_t e;
-  if (n > 1 && launch_flow_jobs(base, jobs, n, stream, &e)) return e;
+  if (n > 1 && launch_flow_jobs(base, jobs, n, stream, &e)) {
+    note_path(1);
+    return e;
+  }
   // SSD jobs of one geometry share the matrix cores' launches (prepass planes
   // per job in the context scratch); others go one by one
   if (n > 1 && launch_mfma_jobs(base, jobs, n, stream, &e)) return e;
   MfmaGeom mg;
   const bool mfma = base.cost_kind == COST_SSD && plan_mfma_ssd(job_args(base, jobs[0]), &mg) &&
-                    (mg.bmv || base.scratch);
-  if (n > 1 && !mfma && launch_item_jobs(base, jobs, n, stream, &e)) return e;
+                    (mg.scratch_bytes == 0 || base.scratch);
+  if (n > 1 && !mfma && launch_item_jobs(base, jobs, n, stream, &e)) {
+    note_path(1);
+    return e;
+  }
   for (int i = 0; i < n; i++) {
     if (jobs[i].r1 <= jobs[i].r0) continue;
     e = launch_search(job_args(base, jobs[i]), stream, nullptr);
@@ -2050,8 +2062,9 @@ hipError_t launch_search(const SearchArgs& p, hipStream_t stream, int* used_fast
   if (used_fast) *used_fast = 0;
   if (p.cost_kind == COST_SSIM) return launch_ssim(p, stream);
   MfmaGeom mg;
+  // (the band-walk and lean kernels need no context scratch: scratch_bytes 0)
   if (p.cost_kind == COST_SSD && plan_mfma_ssd(p, &mg) &&
-      (mg.bmv || (p.scratch && p.scratch_bytes >= mg.scratch_bytes))) {
+      (mg.scratch_bytes == 0 || (p.scratch && p.scratch_bytes >= mg.scratch_bytes))) {
     // Matrix cores: every full-width block (the partial bottom row included);
     // the partial right column stays on the generic kernel.
     hipError_t e = launch_mfma_ssd(p, mg, stream);

@@ -1938,7 +1938,12 @@ static hipError_t launch_bw_jobs(const SearchArgs& p, const MfmaGeom& g, const M
   return launch_bmv(p, t, tj, stream);
 }
 
+static int mfma_path(const SearchArgs& p, const MfmaGeom& g) {
+  return g.bw ? 3 : g.bmv ? 4 : p.blk == 8 ? 6 : g.bm ? 2 : 5;
+}
+
 hipError_t launch_mfma_ssd(const SearchArgs& p, const MfmaGeom& g, hipStream_t stream) {
+  note_path(mfma_path(p, g));
   const MfmaJobs jb = single_job(p, g);
   if (g.bw) return launch_bw_jobs(p, g, jb, stream);
   if (g.bmv) return launch_bmv(p, g, jb, stream);
@@ -2022,6 +2027,7 @@ bool launch_mfma_jobs(const SearchArgs& base, const SearchJob* jobs, int n, hipS
     m = base.scratch ? (int)(base.scratch_bytes / stride) : 0;
   if (g.bw) plan_bw(p, &g, m);  // segments sized for m jobs per launch
   if (m < 2 || g.nbx < p.nbx) return false;  // (a partial right column: job by job)
+  note_path(mfma_path(p, g));
   for (int i0 = 0; i0 < n && *err == hipSuccess; i0 += m) {
     MfmaJobs jb;
     jb.n = n - i0 < m ? n - i0 : m;

@@ -419,6 +419,7 @@ __global__ __launch_bounds__(SSIM_THREADS) void me_ssim_kernel(SearchArgs p, int
 }
 
 hipError_t launch_ssim(const SearchArgs& p, hipStream_t stream) {
+  note_path(7);
   const int rows = p.block_row_end - p.block_row_begin;
   if (rows <= 0 || p.nbx <= 0) return hipSuccess;
   const int B = p.blk;

@@ -45,16 +45,27 @@ def plan_stripes(width: int, height: int, blk: int, span: int, shards: int) -> l
 
 
 def set_kernel_path(path: str) -> None:
-    """'auto': 16x16 and 8x8 SSD on the matrix cores (i8 MFMA), the rest on
-    the VALU kernels; 'valu': VALU kernels only; 'tiles': as 'auto' with 16x16
-    SSD on the 4x4-block-tile MFMA kernel; 'lean': as 'auto' with 16x16 SSD
-    (S <= 64) forming S2 in the search kernel (no prepass planes, no scratch).
-    Process-wide; results are identical."""
+    """'auto': 16x16 and 8x8 SSD on the matrix cores (i8 MFMA; 16x16 with
+    S <= 64 on the band-walk kernel), the rest on the VALU kernels; 'valu':
+    VALU kernels only; 'tiles': as 'auto' with 16x16 SSD on the 4x4-block-tile
+    MFMA kernel; 'lean': as 'auto' with 16x16 SSD (S <= 64) forming S2 per
+    workgroup (me_mfma_bmv_kernel); 'prepass': 16x16 SSD on the S2 prepass +
+    block-major pair.  Process-wide; results are identical."""
     codes = {"auto": _lib.ME_PATH_AUTO, "valu": _lib.ME_PATH_VALU, "tiles": _lib.ME_PATH_MFMA_TILES,
              "lean": _lib.ME_PATH_MFMA_LEAN, "prepass": _lib.ME_PATH_MFMA_PREPASS}
     if path not in codes:
         raise MEError(_lib.ME_EINVAL, f"unknown kernel path {path!r}")
     _lib.lib().me_set_kernel_path(codes[path])
+
+
+SEARCH_PATHS = {0: "none", 1: "valu", 2: "mfma_prepass", 3: "mfma_bandwalk", 4: "mfma_lean",
+                5: "mfma_tiles", 6: "mfma_8x8", 7: "ssim"}
+
+
+def last_search_path() -> str:
+    """The kernel family of the most recent search launched in this process
+    (me_last_search_path): 'valu', 'mfma_prepass', 'mfma_bandwalk', ..."""
+    return SEARCH_PATHS.get(_lib.lib().me_last_search_path(), "unknown")
 
 
 def version() -> str:

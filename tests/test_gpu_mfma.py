@@ -304,6 +304,11 @@ def test_band_walk_segments_and_batches(engine, ssd_path, shape, span):
     pairs = [_pair(rng, h, w, dx=int(rng.integers(-5, 6)), dy=int(rng.integers(-5, 6))) for _ in range(6)]
     ref, cur = pairs[0]
     _check(engine, ref, cur, span, f"{h}x{w} S{span} single")
+    # the automatic path of a single frame is the band-walk kernel (round 5:
+    # a missing scratch check had sent it to the VALU kernels, correct but 3x
+    # slower)
+    engine.full_search(ref, cur, 16, span, "ssd")
+    assert me.last_search_path() == "mfma_bandwalk", me.last_search_path()
     dev = torch.device("cuda", 0)
     nb = me.num_blocks(w, h, 16)
     rt = torch.from_numpy(np.stack([r for r, _ in pairs])).to(dev)
@@ -312,6 +317,7 @@ def test_band_walk_segments_and_batches(engine, ssd_path, shape, span):
     co = torch.empty(6 * nb, dtype=torch.int32, device=dev)
     engine.search_batch_device(rt, 0, ct, 0, w, h, 16, span, "ssd", 0, (h + 15) // 16, mv, co)
     torch.cuda.synchronize()
+    assert me.last_search_path() == "mfma_bandwalk", me.last_search_path()
     mv, co = mv.cpu().numpy().reshape(6, nb, 2), co.cpu().numpy().view(np.uint32).reshape(6, nb)
     for f, (r, c) in enumerate(pairs):
         omv, oc, _ = O.full_search(r, c, 16, span, "ssd", threads=NT)
@@ -354,3 +360,24 @@ def test_band_walk_forced_segment_rows(tmp_path, seg):
                        env=env)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "segments ok" in r.stdout
+
+
+@pytest.mark.parametrize("path,want", [("auto", "mfma_bandwalk"), ("prepass", "mfma_prepass"),
+                                       ("lean", "mfma_lean"), ("tiles", "mfma_tiles"), ("valu", "valu")])
+def test_kernel_path_reported(engine, path, want):
+    """me_last_search_path names the kernel family each me_set_kernel_path
+    value runs for a 16x16 +-32 SSD search (single frame); SAD runs the VALU
+    kernels on every path."""
+    rng = np.random.default_rng(11)
+    ref, cur = _pair(rng, 256, 320, dx=2, dy=-1)
+    try:
+        me.set_kernel_path(path)
+        mv, c = engine.full_search(ref, cur, 16, 32, "ssd")
+        assert me.last_search_path() == want, (path, me.last_search_path())
+        omv, oc, _ = O.full_search(ref, cur, 16, 32, "ssd", threads=NT)
+        np.testing.assert_array_equal(mv, omv)
+        np.testing.assert_array_equal(c, oc)
+        engine.full_search(ref, cur, 16, 32, "sad")
+        assert me.last_search_path() == "valu"
+    finally:
+        me.set_kernel_path("auto")

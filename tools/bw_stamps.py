@@ -36,12 +36,15 @@ for _ in range(20):
 torch.cuda.synchronize()
 L = _lib.lib()
 L.me_debug_bw_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
-buf = np.zeros(8 * 8 * 4096, np.uint64)
+NW = 16  # stamp slots per workgroup (me_band.hip BW_STW)
+buf = np.zeros(NW * 8 * 4096, np.uint64)
 L.me_debug_bw_stamps(buf.ctypes.data, buf.size)
-st = buf.reshape(4096, 8, 8).astype(np.float64)
+st = buf.reshape(4096, NW, 8).astype(np.float64)
 used = st[:, 0, 7] > 0
 st = st[used]
 names = ["prologue", "entries", "fetch", "tiles", "band end", "producer", "barrier"]
+nw = int((st[:, :, 7] > 0).any(axis=0).sum())  # waves of the kernel
+st = st[:, :nw]
 tot = st[:, :, :7].sum(axis=2)
 print(f"{cfg} F={F}: {used.sum()} workgroups, iterations median {np.median(st[:, 0, 7]):.0f}")
 print(f"  wave-lifetime cycles (stamped): median {np.median(tot):.0f}")
@@ -49,6 +52,6 @@ for k, nm in enumerate(names):
     share = st[:, :, k].sum() / tot.sum()
     per_it = np.median(st[:, :, k] / np.maximum(st[:, :, 7], 1))
     print(f"  {nm:9s} {100 * share:5.1f} %  median per iteration {per_it:8.1f} cycles")
-for wv in range(8):
+for wv in range(nw):
     row = " ".join(f"{np.median(st[:, wv, k] / np.maximum(st[:, wv, 7], 1)):7.0f}" for k in range(1, 7))
     print(f"  wave {wv}: per iteration [entries fetch tiles end producer barrier] {row}")
