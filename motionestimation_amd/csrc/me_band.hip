@@ -64,31 +64,20 @@ namespace me {
 namespace {
 
 using mfma::v4i;
-using mfma::lshl6_add;
 using mfma::mfma_job;
 using mfma::opaque;
 using mfma::umin3;
 
-constexpr int BW_RAWN = 6;           // raw slab ring (slabs b + 1 .. b + 6 at band b)
 constexpr int BW_OPS = 46;           // producer steps per band: 16 rows in, then 15 x (out, in)
-
-// The rings of a workgroup with PW producer waves: band m is produced over the
-// PW iterations before it is searched (phase t in iteration m - PW + t).
-template <int PW>
-struct BwRings {
-  static constexpr int IT = (BW_OPS + PW - 1) / PW;  // producer steps per iteration
-  static constexpr int P0N = PW + 1;                 // P0 planes: the band searched + PW in production
-  static constexpr int XR = PW + 1;                  // XOR-ed slab ring (slab s in slot s % XR)
-  static constexpr int XN = XR + 1;                  // + the mirror of slot 0
-  static constexpr int E = IT > 16 ? 1 : 0;          // phase 0 also reads slab m + 1
-};
 constexpr int BW_CREC = 48;          // cur row record: 16 zero bytes, the row (c ^ 0x7F), 16 zero bytes
+constexpr int BW_NSW = 12;           // searcher waves per workgroup (three per SIMD)
+constexpr int BW_PW = 4;             // producer waves per workgroup (one per SIMD)
 
 #ifdef ME_STAMPS
 // Diagnostic build only (libme_hip_stamps.so): per workgroup and wave, the
-// s_memtime cycles spent in each phase of the band loop, summed over the
-// iterations: [prologue, entries / slab DMA + XOR, fetch, tiles, band end,
-// production, barrier wait, iterations] (tools/bw_stamps.py).
+// s_memtime cycles spent in each phase, summed over the bands: [start,
+// entries / producer's slot wait, fetch, tiles, band end, production, ready
+// wait, bands] (tools/bw_stamps.py).
 constexpr int BW_STW = 16;  // waves per workgroup slot
 __device__ unsigned long long g_bwstamps[BW_STW * 8 * 4096];
 #define BW_T0() unsigned long long bw_t = __builtin_amdgcn_s_memtime()
@@ -97,6 +86,18 @@ __device__ unsigned long long g_bwstamps[BW_STW * 8 * 4096];
 #define BW_T0() do { } while (0)
 #define BW_ACC(k) do { } while (0)
 #endif
+
+constexpr int BW_K = 8;              // band ring: the bands in flight (window + P0 plane each)
+constexpr int BW_WIN_ROWS = 31;      // window rows of a band: 16 b .. 16 b + 30
+
+// Producer -> searcher handshake per band slot (LDS): ready[k] = the band
+// whose window and P0 plane slot k holds (published after they are written);
+// done[k] = searcher waves finished with it (the producer of band b + K
+// waits for all of them, then reuses the slot).
+struct BwCtl {
+  int ready[BW_K];
+  int done[BW_K];
+};
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) const uint32_t lds_c32;
@@ -112,50 +113,52 @@ __device__ __forceinline__ v4i ldv4(uint32_t a) {
   return *reinterpret_cast<lds_cv4i*>((uintptr_t)a);
 }
 
-// LDS layout (bytes): XN slabs | RAWN slabs | P0N planes | crec (searchers) | keys
-__host__ __device__ constexpr int bw_slab(int lp) { return 16 * lp; }
-__host__ __device__ inline int bw_lds_bytes(int lp, int pp, int ns, int nsw, int pw) {
-  return (pw + 2 + BW_RAWN) * bw_slab(lp) + (pw + 1) * 16 * pp * 4 + nsw * 16 * BW_CREC + nsw * ns * 8;
+// LDS layout (bytes): K windows | K P0 planes | crec (searchers) | keys | ctl
+__host__ __device__ constexpr int bw_win(int lp) { return BW_WIN_ROWS * lp; }
+__host__ __device__ inline int bw_lds_bytes(int lp, int pp, int ns, int nsw) {
+  return BW_K * bw_win(lp) + BW_K * 16 * pp * 4 + nsw * 16 * BW_CREC + nsw * ns * 8 + (int)sizeof(BwCtl);
 }
 
-// Waits until at most n of this wave's vector-memory operations are
-// outstanding (s_waitcnt takes an immediate).
-__device__ __forceinline__ void wait_vm(int n) {
-  switch (n) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
-    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+// Bounded spin on an LDS word (the handshake's ordering argument says it
+// ends; the bound keeps a broken invariant from hanging the GPU: an expired
+// wait sets the context's error word, read back as ME_EDEVICE).
+template <typename Pred>
+__device__ __forceinline__ bool bw_wait(const SearchArgs& p, int lane, Pred ok) {
+  int spins = 0;
+  while (!ok()) {
+    if (++spins >= (1 << 22)) {
+      if (lane == 0 && p.sched)
+        __hip_atomic_store(p.sched + SCHED_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
   }
+  return true;
 }
 
-// NSW searcher waves + PW producer waves; <= 128 VGPRs (four waves per SIMD:
-// one workgroup of 16 waves, or two of 8, per CU)
+// NSW searcher waves + PW producer waves, <= 128 VGPRs (four waves per SIMD).
+// No workgroup barrier after the start: bands flow through a ring of BW_K
+// slots, each published by its producer and released by its searchers, so a
+// wave's band-end work and its waits overlap the MFMAs of the SIMD's other
+// waves instead of every wave meeting at a barrier each band.
 template <int C, int NS, int LP, int NSW, int PW, bool ABL>
 __global__ __launch_bounds__(64 * (NSW + PW), 4) void me_mfma_bw_kernel(SearchArgs p, MfmaGeom g, MfmaJobs jb) {
-  using R = BwRings<PW>;
-  constexpr int BW_P0N = R::P0N, BW_XR = R::XR, BW_XN = R::XN, BW_OPS_IT = R::IT;
   constexpr int WPC = NSW / C;  // row classes per column
-  constexpr int SLAB = bw_slab(LP);
-  // DMA instructions of this wave per slab (1,024 bytes each, dealt round the producers)
+  constexpr int WIN = bw_win(LP);
   extern __shared__ __align__(16) uint8_t smem[];
   const int PP = g.bw_pp;
   const int P0PLANE = 16 * PP;  // ints
   uint8_t* xw = smem;
-  uint8_t* raw = xw + BW_XN * SLAB;
-  int* p0 = reinterpret_cast<int*>(raw + BW_RAWN * SLAB);
-  uint8_t* crec_all = reinterpret_cast<uint8_t*>(p0 + BW_P0N * P0PLANE);
+  int* p0 = reinterpret_cast<int*>(xw + BW_K * WIN);
+  uint8_t* crec_all = reinterpret_cast<uint8_t*>(p0 + BW_K * P0PLANE);
   unsigned long long* keys = reinterpret_cast<unsigned long long*>(crec_all + NSW * 16 * BW_CREC);
+  BwCtl* ctl = reinterpret_cast<BwCtl*>(keys + NSW * NS);
 
   const int tid = (int)threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const bool searcher = wave < NSW;
-  const int col = wave % C, cls = wave / C;                // searchers
-  const int pw = wave - NSW;                               // producers: index
-  const int nps = pw >= 0 && pw * 1024 < SLAB ? (SLAB - pw * 1024 + PW * 1024 - 1) / (PW * 1024) : 0;
+  const int col = wave % C, cls = wave / C;  // searchers
+  const int pw = wave - NSW;                 // producers: index
   const int n = lane & 15, h = lane >> 4;
   const int S = p.range, W = p.width, H = p.height;
   int lin = mfma::xcd_banded_index();
@@ -176,27 +179,15 @@ __global__ __launch_bounds__(64 * (NSW + PW), 4) void me_mfma_bw_kernel(SearchAr
   auto hi = [&](int br) { return min(16 * br + S, H - 16) >> 4; };  // last band of row br
   auto E = [&](int b) { return b <= 0 ? 0 : b + Sc; };              // first row with lo >= b
   const int bfirst = lo(r0), blast = hi(r1 - 1);
-  const int bend = blast + 1;  // slabs bfirst .. bend are read (band blast's window reaches slab bend)
+  const int nact = WPC * ncol;  // searcher waves that walk the bands (a column each)
 
   // ================================ producers
-  // the window: raw slabs by LDS DMA (frame rows [16 s, 16 s + 16) x columns
-  // [16 tc0, 16 tc0 + LP)).  Rows outside the resident ones are outside the
-  // buffer range and read as 0 (their positions are masked).
+  // Window rows straight from global memory (8 bytes per lane: the 4
+  // positions of group pg and the 4 bytes after them), rows outside the
+  // resident ones outside the buffer range (read as 0; their positions are
+  // masked).
   const __amdgpu_buffer_rsrc_t rref =
       __builtin_amdgcn_make_buffer_rsrc((void*)p.ref, (short)0, p.ref_bytes, 0x00020000);
-  auto dma_slab = [&](int s) {
-    uint8_t* dst = raw + (s % BW_RAWN) * SLAB;
-    const int rowb = 16 * s - p.ref_row0;
-    for (int s0 = pw * 1024; s0 < SLAB; s0 += PW * 1024) {
-      const int d = s0 + 16 * lane;
-      if (d < SLAB) {
-        const int rho = d / LP, k = d - rho * LP;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            rref, (__attribute__((address_space(3))) void*)(dst + s0), 16,
-            (uint32_t)((rowb + rho) * p.stride + 16 * tc0 + k), 0, 0, 0);
-      }
-    }
-  };
   // V(row) = sum of 16 window rows of H, H(row, x) = sum over the 4 bytes at
   // x of (r - 127)^2 (u = r ^ 0x7F = 127 - r as an i8: one v_dot4 per 4
   // bytes).  Lane (row R, l) owns the 4 positions of group pg = 13 R + l: the
@@ -205,7 +196,7 @@ __global__ __launch_bounds__(64 * (NSW + PW), 4) void me_mfma_bw_kernel(SearchAr
   const int pg = 13 * (lane >> 4) + (lane & 15);
   const bool pout = (lane & 15) < 13 && 4 * pg < npos;
   const bool pxor = (lane & 15) < 13 && 4 * pg < LP;  // writes the XOR-ed window bytes 4 pg .. 4 pg + 3
-  v4i V = {0, 0, 0, 0};
+  v4i V = {0, 0, 0, 0}, R = {0, 0, 0, 0};  // sums of the rows added / removed
   auto h_acc = [&](uint32_t w0, uint32_t w1, v4i acc) {  // acc + H of the bytes (w0, w1)
     const uint32_t u0 = w0 ^ 0x7F7F7F7Fu, u1 = w1 ^ 0x7F7F7F7Fu;
     const uint32_t u[4] = {u0, __builtin_amdgcn_alignbyte(u1, u0, 1),
@@ -215,107 +206,92 @@ __global__ __launch_bounds__(64 * (NSW + PW), 4) void me_mfma_bw_kernel(SearchAr
     for (int r = 0; r < 4; r++) acc[r] = __builtin_amdgcn_sdot4((int)u[r], (int)u[r], acc[r], false);
     return acc;
   };
-  // row j of band m: S2(x) = V(x) + V(x + 4) + V(x + 8) + V(x + 12), the
+  // row j of the band in slot k: with D = V - R (the rows added minus the
+  // rows removed), S2(x) = D(x) + D(x + 4) + D(x + 8) + D(x + 12), the
   // neighbours by DPP row_shl 1 then 2; stored as the key's position term
-  auto out_row = [&](int m, int j) {
-    v4i T, Q;
+  // P0 = (S2 << 6) + 2^29 + 64 + idx, idx = 4 (tile - tc0) + (x & 3): the
+  // strip-relative tile, so the search adds nothing per tile (a lane's keys
+  // share its x & 12, and idx orders its candidates by x)
+  const uint32_t p0k = (1u << 29) + 64u + 4u * (uint32_t)(pg >> 2);
+  auto out_row = [&](int k, int j) {
+    v4i T, Q, D;
 #pragma unroll
-    for (int r = 0; r < 4; r++) T[r] = V[r] + __builtin_amdgcn_update_dpp(0, V[r], 0x101, 0xF, 0xF, false);
+    for (int r = 0; r < 4; r++) D[r] = V[r] - R[r];
+#pragma unroll
+    for (int r = 0; r < 4; r++) T[r] = D[r] + __builtin_amdgcn_update_dpp(0, D[r], 0x101, 0xF, 0xF, false);
 #pragma unroll
     for (int r = 0; r < 4; r++) Q[r] = T[r] + __builtin_amdgcn_update_dpp(0, T[r], 0x102, 0xF, 0xF, false);
     if (pout) {
       v4i o;
 #pragma unroll
-      for (int r = 0; r < 4; r++) o[r] = (int)lshl6_add((uint32_t)Q[r], (1u << 29) + 64u + (uint32_t)r);
+      for (int r = 0; r < 4; r++) o[r] = (int)(((uint32_t)Q[r] << 6) + p0k + (uint32_t)r);
       // the lane's base recomputed per row (opaque): hoisted, the 16 row
       // addresses pinned 16 VGPRs and spilled
       typedef __attribute__((address_space(3))) v4i lds_v4i;
-      const uint32_t pa = (uint32_t)opaque((int)lds_addr(p0 + 4 * pg)) +
-                          4u * (uint32_t)((m % BW_P0N) * P0PLANE + j * PP);
+      const uint32_t pa = (uint32_t)opaque((int)lds_addr(p0 + 4 * pg)) + 4u * (uint32_t)(k * P0PLANE + j * PP);
       *reinterpret_cast<lds_v4i*>((uintptr_t)pa) = o;
     }
   };
-  // Steps [O0, O1) of band m (compile-time, at most 12): 0..15 add rows
-  // 0..15 (row 0 out after 15), then for j = 1..15: remove row j - 1, add
-  // row j + 15, row j out.  Straight-line code; the window rows of all the
-  // steps are read first (one LDS latency).  Steps 0..15 read slab m's rows
-  // once, so they also store them XOR-ed with 0x80 (r - 128 as an i8: the
-  // MFMA B operand) into ring slot m % XR, and slot 0 into the mirror after
-  // slot XR - 1: band b's rows 16 b .. 16 b + 30 are then contiguous from
-  // slot b % XR.  Band m is produced in iterations m - PW .. m - 1 of the
-  // walk; the slot's previous slab (m - XR) was last read by band m - XR.
-  // Band m > blast (the last slab, bend) runs the phases with steps below 16
-  // for the XOR only (no P0 rows).
-  auto steps = [&](auto c0, auto c1, int m) __attribute__((always_inline)) {
-    constexpr int O0 = decltype(c0)::value;
-    constexpr int O1 = decltype(c1)::value;
-    const bool outp = m <= blast;
-    const uint32_t xa = lds_addr(xw + (m % BW_XR) * SLAB) + 4u * (uint32_t)pg;
-    const bool mirror = m % BW_XR == 0;
+  // The band's window rows (16 m .. 16 m + 30, LP bytes from column 16 tc0)
+  // by LDS DMA straight into its slot, then XOR-ed there in place by the
+  // production below.  DMA_N instructions of 64 lanes x 16 bytes per window.
+  constexpr int DMA_N = (WIN + 1023) / 1024;
+  auto dma_win = [&](int m, int k) __attribute__((always_inline)) {
+    uint8_t* dst = xw + k * WIN;
+    const int rowb = 16 * m - p.ref_row0;
+#pragma unroll
+    for (int i = 0; i < DMA_N; i++) {
+      const int d = 1024 * i + 16 * lane;
+      if (d < WIN) {  // lane 0 always: every instruction issues (vmcnt counts DMA_N)
+        const int rho = d / LP, kk = d - rho * LP;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rref, (__attribute__((address_space(3))) void*)(dst + 1024 * i), 16,
+            (uint32_t)((rowb + rho) * p.stride + 16 * tc0 + kk), 0, 0, 0);
+      }
+    }
+  };
+  // Band m's 46 steps: 0..15 add window rows 0..15 (row 0 out after 15), then
+  // for j = 1..15: remove row j - 1, add row j + 15, row j out.  Every "add"
+  // step reads its row raw and writes it back XOR-ed with 0x80 (r - 128 as an
+  // i8: the MFMA B operand; the lanes read the row before any writes it, and
+  // lanes l < 13 hold each 4 bytes once); a "remove" step reads its row
+  // XOR-ed (u = r ^ 0x7F = w ^ 0xFF).  Steps [O0, O1) (compile-time, at most
+  // 12): the rows of all the steps are read first (one LDS latency).
+  auto step_row = [](int o) { return o < 16 ? o : ((o - 16) & 1) ? ((o - 16) >> 1) + 16 : ((o - 16) >> 1); };
+  auto steps = [&](auto c0, auto c1, int k) __attribute__((always_inline)) {
+    constexpr int O0 = decltype(c0)::value, O1 = decltype(c1)::value;
+    typedef __attribute__((address_space(3))) uint32_t lds_u32;
+    const uint32_t xa = (uint32_t)opaque((int)lds_addr(xw + k * WIN)) + 4u * (uint32_t)pg;
     uint32_t w0[12], w1[12];
 #pragma unroll
     for (int o = O0; o < O1; o++) {
-      const int q = o - 16;
-      const int rho = o < 16 ? o : (q & 1) ? (q >> 1) + 16 : (q >> 1);
-      const uint32_t a = lds_addr(raw + ((m + (rho >> 4)) % BW_RAWN) * SLAB + (rho & 15) * LP) +
-                         4u * (uint32_t)pg;
-      w0[o - O0] = ld32(a);
-      w1[o - O0] = ld32(a + 4);
+      w0[o - O0] = ld32(xa + (uint32_t)(step_row(o) * LP));
+      w1[o - O0] = ld32(xa + (uint32_t)(step_row(o) * LP + 4));
     }
 #pragma unroll
     for (int o = O0; o < O1; o++) {
-      const int k = o - O0;
+      const bool add = o < 16 || ((o - 16) & 1);
+      const uint32_t x0 = w0[o - O0], x1 = w1[o - O0];
+      if (add && pxor) *reinterpret_cast<lds_u32*>((uintptr_t)(xa + (uint32_t)(step_row(o) * LP))) = x0 ^ 0x80808080u;
       if (o < 16) {
-        if (pxor) {
-          typedef __attribute__((address_space(3))) uint32_t lds_u32;
-          const uint32_t xv = w0[k] ^ 0x80808080u;
-          *reinterpret_cast<lds_u32*>((uintptr_t)(xa + (uint32_t)(o * LP))) = xv;
-          if (mirror) *reinterpret_cast<lds_u32*>((uintptr_t)(xa + (uint32_t)(BW_XR * SLAB + o * LP))) = xv;
-        }
         const v4i z = {0, 0, 0, 0};
-        V = h_acc(w0[k], w1[k], o == 0 ? z : V);
-        if (o == 15 && outp) out_row(m, 0);
+        V = h_acc(x0, x1, o == 0 ? z : V);
+        if (o == 0) R = z;
+        if (o == 15) out_row(k, 0);
+      } else if (!add) {
+        R = h_acc(x0 ^ 0x80808080u, x1 ^ 0x80808080u, R);
       } else {
-        const int q = o - 16, j = (q >> 1) + 1;
-        if ((q & 1) == 0) {
-          const v4i z = {0, 0, 0, 0};
-          V -= h_acc(w0[k], w1[k], z);
-        } else {
-          V = h_acc(w0[k], w1[k], V);
-          if (outp) out_row(m, j);
-        }
+        V = h_acc(x0, x1, V);
+        out_row(k, ((o - 16) >> 1) + 1);
       }
     }
   };
-  // phase T of band m: steps [IT T, min(IT T + IT, 46)), in chunks of 12
-  auto produce = [&](auto tc, int m) __attribute__((always_inline)) {
-    constexpr int T = decltype(tc)::value;
-    constexpr int O0 = BW_OPS_IT * T;
-    constexpr int O1 = O0 + BW_OPS_IT < BW_OPS ? O0 + BW_OPS_IT : BW_OPS;
-    constexpr int O2 = O0 + 12 < O1 ? O0 + 12 : O1;
-    steps(std::integral_constant<int, O0>{}, std::integral_constant<int, O2>{}, m);
-    if constexpr (O2 < O1) {
-      constexpr int O3 = O2 + 12 < O1 ? O2 + 12 : O1;
-      steps(std::integral_constant<int, O2>{}, std::integral_constant<int, O3>{}, m);
-      static_assert(O3 == O1, "at most two chunks per phase");
-    }
+  auto produce = [&](int k) __attribute__((always_inline)) {
+    steps(std::integral_constant<int, 0>{}, std::integral_constant<int, 12>{}, k);
+    steps(std::integral_constant<int, 12>{}, std::integral_constant<int, 24>{}, k);
+    steps(std::integral_constant<int, 24>{}, std::integral_constant<int, 36>{}, k);
+    steps(std::integral_constant<int, 36>{}, std::integral_constant<int, BW_OPS>{}, k);
   };
-  auto produce_phase = [&](int t, int m) __attribute__((always_inline)) {
-    if constexpr (PW == 2) {
-      if (t == 0) produce(std::integral_constant<int, 0>{}, m);
-      else produce(std::integral_constant<int, 1>{}, m);
-    } else {
-      switch (t) {
-        case 0: produce(std::integral_constant<int, 0>{}, m); break;
-        case 1: produce(std::integral_constant<int, 1>{}, m); break;
-        case 2: produce(std::integral_constant<int, 2>{}, m); break;
-        default: produce(std::integral_constant<int, 3>{}, m); break;
-      }
-    }
-  };
-  // phases of band m == bend (the XOR of the last slab only): those with
-  // steps below 16
-  constexpr int XPH = (15 / BW_OPS_IT) + 1;
 
   // ================================ searchers
   // block rows in flight: a ring of NS slots (this searcher's class)
@@ -339,8 +315,8 @@ __global__ __launch_bounds__(64 * (NSW + PW), 4) void me_mfma_bw_kernel(SearchAr
   const uint8_t* cur_lane = p.cur + (ptrdiff_t)(lane - p.cur_row0) * p.stride + 16 * (bc0 + col);
 
   // The first row entering at band b (this column and class) is prefetched
-  // into pf0 one iteration ahead; further ones (frame top, segment starts)
-  // are loaded when they enter.
+  // into pf0 a band ahead; further ones (frame top, segment starts) are
+  // loaded when they enter.
   u32x4 pf0 = {0u, 0u, 0u, 0u};
   int pe0 = 0, pe1 = 0;  // this class's entering rows: pe0, pe0 + WPC, ... < pe1
   auto fetch = [&](int b) {
@@ -412,7 +388,7 @@ __global__ __launch_bounds__(64 * (NSW + PW), 4) void me_mfma_bw_kernel(SearchAr
     if (hk < (1u << 25)) {
       const uint32_t cost = hk - 1u - (1u << 23) + (uint32_t)cc[s];
       const int idx = (int)(kb & 63u);
-      const int dx = 16 * (i0c + (idx >> 2)) + 4 * h + (idx & 3) - bx;
+      const int dx = 16 * (tc0 + (idx >> 2)) + 4 * h + (idx & 3) - bx;
       const int dy = 16 * bb[s] + n - 16 * br;
       const unsigned long long key = ((unsigned long long)cost << 32) |
                                      ((uint32_t)(dy + 32768) << 16) | (uint32_t)(dx + 32768);
@@ -431,87 +407,84 @@ __global__ __launch_bounds__(64 * (NSW + PW), 4) void me_mfma_bw_kernel(SearchAr
 #ifdef ME_STAMPS
   unsigned long long bw_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
-  if (ABL && (g.bw_abl & 16)) {
-    if (!searcher) __builtin_amdgcn_s_setprio(1);
-  } else if (ABL && (g.bw_abl & 32)) {
-    if (searcher) __builtin_amdgcn_s_setprio(1);
-  }
   BW_T0();
-  // ---- prologue: the first slabs, the keys, the first two XOR-ed slabs, the
-  // production steps the schedule puts before iteration 0, the first rows
-  if (!searcher)
-    for (int s = bfirst; s < bfirst + BW_RAWN && s <= bend; s++) dma_slab(s);
   if (tid < NSW * NS) keys[tid] = ~0ull;
-  if (searcher) fetch(bfirst);
-  // The DMA ring runs ahead: production in iteration b reads raw slabs up to
-  // b + PW + E, so a producer waits only for its DMAs of the slabs up to the
-  // ones it reads next (nps DMA instructions per slab and wave, in order),
-  // not for the ones just issued.  The prologue's production reads slabs up
-  // to bfirst + PW - 1 + E.
-  const int dlast = min(bfirst + BW_RAWN - 1, bend);  // the prologue's DMAs: slabs bfirst .. dlast
-  if (!searcher) wait_vm(nps * max(0, dlast - (bfirst + PW - 1 + R::E)));
-  __syncthreads();
-  if (!searcher) {
-    if (bfirst + pw <= bend && !(ABL && (g.bw_abl & 1))) {
-      const int tend = bfirst + pw <= blast ? PW - pw : min(PW - pw, XPH);
-      for (int t = 0; t < tend; t++) produce_phase(t, bfirst + pw);
-    }
-    wait_vm(nps * max(0, dlast - (bfirst + PW + R::E)));  // iteration 0's slabs
-  } else if (hascol && !(ABL && (g.bw_abl & 4))) {
-    for (int br = pe0; br < pe1; br += WPC)
-      enter(br, br == pe0 ? pf0 : *reinterpret_cast<const u32x4*>(cur_lane + (ptrdiff_t)(16 * br) * p.stride));
+  if (tid < BW_K) {
+    ctl->ready[tid] = -(1 << 30);
+    ctl->done[tid] = 0;
   }
-  __syncthreads();
+  __syncthreads();  // the only barrier: keys and handshake words initialised
   BW_ACC(0);
 
-  const int nit = blast - bfirst + 1;
-  // Two loops, one per role, each with one barrier per band: the searchers'
-  // ring (A fragments, bests) is not live in the producers' loop.
   if (!searcher) {
-    for (int it = 0; it < nit; it++) {
-      const int b = bfirst + it;
-      if (b + BW_RAWN <= bend) dma_slab(b + BW_RAWN);
+    // Producer pw: bands bfirst + pw, + PW, ... in order, each into slot
+    // m % K.  Band m + PW's window is DMA'd (its slot released by every
+    // searcher first) before band m is produced, so the DMA latency hides
+    // behind one band's production.
+    auto claim = [&](int m) {  // wait until slot m % K is free, then DMA band m into it
+      const int k = m % BW_K;
+      if (m - BW_K >= bfirst) {
+        if (!bw_wait(p, lane, [&] {
+              return __hip_atomic_load(&ctl->done[k], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= nact;
+            }))
+          return false;
+        if (lane == 0) __hip_atomic_store(&ctl->done[k], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      dma_win(m, k);
+      return true;
+    };
+    bool ok = bfirst + pw > blast || claim(bfirst + pw);
+#pragma unroll 1
+    for (int m = bfirst + pw; ok && m <= blast; m += PW) {
+      const int k = m % BW_K;
+      const bool next = m + PW <= blast;
+      if (next) ok = claim(m + PW);
       BW_ACC(1);
-      // band b + 1 + d, d = (pw - it - 1) mod PW, its phase PW - 1 - d
-      const int d = ((pw - it - 1) % PW + PW) % PW;
-      const int m = b + 1 + d, t = PW - 1 - d;
-      if ((m <= blast || (m == bend && t < XPH)) && !(ABL && (g.bw_abl & 1))) produce_phase(t, m);
+      // band m's window landed (band m + PW's DMA may still be in flight)
+      if (next)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DMA_N) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (!(ABL && (g.bw_abl & 1))) produce(k);
       BW_ACC(5);
-      // the slabs iteration b + 1 reads (up to b + 1 + PW + E) landed; the
-      // later ones may still be in flight
-      wait_vm(nps * max(0, min(b + BW_RAWN, bend) - (b + 1 + PW + R::E)));
-      __syncthreads();
-      BW_ACC(6);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the window and P0 stores landed
+      if (lane == 0) __hip_atomic_store(&ctl->ready[k], m, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
-  } else {
-  for (int it = 0; it < nit; it++) {
-    const int b = bfirst + it;
-    if (hascol) {
+  } else if (hascol) {
+    fetch(bfirst);
+    if (!(ABL && (g.bw_abl & 4)))
+      for (int br = pe0; br < pe1; br += WPC)
+        enter(br, br == pe0 ? pf0 : *reinterpret_cast<const u32x4*>(cur_lane + (ptrdiff_t)(16 * br) * p.stride));
+#pragma unroll 1
+    for (int b = bfirst; b <= blast; b++) {
+      const int k = b % BW_K;
       // the rows entering at band b + 1: their cur rows load during this
-      // band's tiles, they enter after its end (a wave that finishes its
-      // tiles early does its entries while the SIMD's other waves still run
-      // MFMAs, instead of every wave at the start of the band)
+      // band's tiles, they enter after its end
       if (b + 1 <= blast) fetch(b + 1);
       BW_ACC(2);
-      if (!(ABL && (g.bw_abl & 2))) {
-        // y validity per row in flight: a lane forms the keys of one candidate
-        // row (y = 16 b + n) only, so a row outside the block's range (the
-        // range's partial bands) drops the lane's band best at the band end
-        bool act[NS], yok[NS];
+      if (!bw_wait(p, lane, [&] {
+            return __hip_atomic_load(&ctl->ready[k], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == b;
+          }))
+        break;
+      BW_ACC(6);
+      // y validity per row in flight: a lane forms the keys of one candidate
+      // row (y = 16 b + n) only, so a row outside the block's range (the
+      // range's partial bands) drops the lane's band best at the band end
+      bool act[NS], yok[NS];
 #pragma unroll
-        for (int s = 0; s < NS; s++) {
-          act[s] = srow[s] >= 0;
-          const int ylo = max(16 * srow[s] - S, 0), yhi = min(16 * srow[s] + S, H - 16);
-          const int y = 16 * b + n;
-          yok[s] = y >= ylo && y <= yhi;
-        }
+      for (int s = 0; s < NS; s++) {
+        act[s] = srow[s] >= 0;
+        const int ylo = max(16 * srow[s] - S, 0), yhi = min(16 * srow[s] + S, H - 16);
+        const int y = 16 * b + n;
+        yok[s] = y >= ylo && y <= yhi;
+      }
+      if (!(ABL && (g.bw_abl & 2))) {
         // the tiles of the band for the active slots M (compile-time: no MFMA
         // for a free slot)
         auto tiles = [&](auto mc) __attribute__((always_inline)) {
           constexpr int M = decltype(mc)::value;
-          const uint32_t xb = lds_addr(xw + (b % BW_XR) * SLAB) +
-                              (uint32_t)((n + (h >> 1)) * LP + 16 * (h & 1) - 16 * tc0);
-          const uint32_t pb = lds_addr(p0 + (b % BW_P0N) * P0PLANE) + (uint32_t)((n * PP + 4 * h - 16 * tc0) * 4);
+          const uint32_t xb = lds_addr(xw + k * WIN) + (uint32_t)((n + (h >> 1)) * LP + 16 * (h & 1) - 16 * tc0);
+          const uint32_t pb = lds_addr(p0 + k * P0PLANE) + (uint32_t)((n * PP + 4 * h - 16 * tc0) * 4);
           // fragments through a ring of 4 registers, three fragments ahead
           // (fragment q of tile i: window row n + 2 q + (h >> 1), column 16 i + 16 (h & 1))
           v4i f[4];
@@ -539,10 +512,9 @@ __global__ __launch_bounds__(64 * (NSW + PW), 4) void me_mfma_bw_kernel(SearchAr
               for (int s = 0; s < NS; s++)
                 if ((M >> s) & 1) acc[s] = MFMA16(A[s][q], f[q & 3], q == 0 ? zero4 : acc[s], 0, 0, 0);
             }
-            const uint32_t rel4 = 4u * (uint32_t)(i - i0c);
             uint32_t P[4];
 #pragma unroll
-            for (int r = 0; r < 4; r++) P[r] = (uint32_t)pv[r] + rel4;
+            for (int r = 0; r < 4; r++) P[r] = (uint32_t)pv[r];
             if constexpr (E) {
 #pragma unroll
               for (int r = 0; r < 4; r++) {
@@ -585,36 +557,36 @@ __global__ __launch_bounds__(64 * (NSW + PW), 4) void me_mfma_bw_kernel(SearchAr
         } else {
           if (am) tiles(std::integral_constant<int, (1 << NS) - 1>{});
         }
-        BW_ACC(3);
-        // band end: the lane's best of the band into the row's best (an earlier
-        // band keeps ties: smaller dy); rows whose last band this was leave
-#pragma unroll
-        for (int s = 0; s < NS; s++) {
-          if (!act[s]) continue;
-          if (yok[s] && (bcur[s] >> 6) < (bk[s] >> 6)) {
-            bk[s] = bcur[s];
-            bb[s] = b;
-          }
-          bcur[s] = ~0u;
-          if (hi(srow[s]) == b) {
-            emit(s);
-            srow[s] = -1;
-          }
-        }
-        BW_ACC(4);
       }
+      // band b's LDS reads are done: release the slot
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (lane == 0) __hip_atomic_fetch_add(&ctl->done[k], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      BW_ACC(3);
+      // band end: the lane's best of the band into the row's best (an earlier
+      // band keeps ties: smaller dy); rows whose last band this was leave
+#pragma unroll
+      for (int s = 0; s < NS; s++) {
+        if (!act[s]) continue;
+        if (yok[s] && (bcur[s] >> 6) < (bk[s] >> 6)) {
+          bk[s] = bcur[s];
+          bb[s] = b;
+        }
+        bcur[s] = ~0u;
+        if (hi(srow[s]) == b) {
+          emit(s);
+          srow[s] = -1;
+        }
+      }
+      BW_ACC(4);
       if (b + 1 <= blast && !(ABL && (g.bw_abl & 4)))
         for (int br = pe0; br < pe1; br += WPC)
           enter(br, br == pe0 ? pf0 : *reinterpret_cast<const u32x4*>(cur_lane + (ptrdiff_t)(16 * br) * p.stride));
       BW_ACC(1);
     }
-    __syncthreads();
-    BW_ACC(6);
-  }
   }
 #ifdef ME_STAMPS
   if (lane == 0 && blockIdx.x < 4096) {
-    bw_acc[7] = (unsigned long long)nit;
+    bw_acc[7] = (unsigned long long)(blast - bfirst + 1);
     for (int k = 0; k < 8; k++) g_bwstamps[(blockIdx.x * BW_STW + wave) * 8 + k] = bw_acc[k];
   }
 #endif
@@ -649,17 +621,12 @@ bool plan_bw(const SearchArgs& p, MfmaGeom* g, int jobs) {
   const int rows = g->nrows - (g->hb_row >= 0 ? 1 : 0);       // full-height rows
   if (rows < 1 || g->nbx < 1) return false;
   // Two ring slots per searcher wave (A fragments of 2 rows: 64 VGPRs): the
-  // 2 ceil(S/16) + 1 rows in flight of a column split over nsw / C
-  // searchers, the widest strip whose column fits its rows.  Two shapes, both
-  // four waves per SIMD at <= 128 VGPRs:
-  //   - one workgroup of 12 searchers + 4 producers (the default):
-  //     S <= 16: 6 columns; S <= 32: 4; S <= 48: 3; S <= 64: 2;
-  //   - two workgroups per CU of 6 searchers + 2 producers (ME_BW_WG=2,
-  //     tuning build): S <= 16: 3 columns; S <= 32: 2; S <= 64: 1.  Measured
-  //     slower at 1080p (32.4 against 27.9 us per frame of a 16-frame batch,
-  //     equal at 4K: profiles/r05w_ssd_ab.jsonl).
-  const bool big = tuning().bw_wg != 2;
-  const int nsw = big ? 12 : 6, npw = big ? 4 : 2, ns = 2, wgs_cu = big ? 1 : 2;
+  // 2 ceil(S/16) + 1 rows in flight of a column split over 12 / C searchers,
+  // the widest strip whose column fits its rows: S <= 16: 6 columns (3 rows
+  // on 4 slots); S <= 32: 4 (5 on 6); S <= 48: 3 (7 on 8); S <= 64: 2 (9 on
+  // 12).  One workgroup of 12 searchers + 4 producers per CU (four waves per
+  // SIMD at <= 128 VGPRs).
+  const int nsw = BW_NSW, npw = BW_PW, ns = 2, wgs_cu = 1;
   const int inflight = 2 * ((S + 15) / 16) + 1;
   int C = 0;
   for (int c : {6, 4, 3, 2, 1})
@@ -699,7 +666,7 @@ bool plan_bw(const SearchArgs& p, MfmaGeom* g, int jobs) {
   g->bw_seg_rows = best_l;
   g->bw_abl = tuning().bw_abl;
   g->bw_segs = (rows + best_l - 1) / best_l;
-  g->lds = bw_lds_bytes(lp, pp, ns, nsw, npw);
+  g->lds = bw_lds_bytes(lp, pp, ns, nsw);
   if (g->lds > 160 * 1024 / wgs_cu) return false;
   g->bw = 1;
   return true;
@@ -725,8 +692,6 @@ hipError_t launch_bw(const SearchArgs& p, const MfmaGeom& g0, const MfmaJobs& jb
       hipLaunchKernelGGL((me_mfma_bw_kernel<C, NS, LP, NSW, PW, false>), grid, blk, g.lds, stream, p, g, jb); \
     return hipGetLastError();                                                                   \
   }
-  ME_BW_CASE(3, 2, 160, 6, 2) ME_BW_CASE(2, 2, 160, 6, 2) ME_BW_CASE(1, 2, 160, 6, 2)
-  ME_BW_CASE(1, 2, 224, 6, 2)
   ME_BW_CASE(6, 2, 160, 12, 4) ME_BW_CASE(4, 2, 160, 12, 4) ME_BW_CASE(3, 2, 160, 12, 4)
   ME_BW_CASE(3, 2, 224, 12, 4) ME_BW_CASE(2, 2, 160, 12, 4) ME_BW_CASE(2, 2, 224, 12, 4)
 #undef ME_BW_CASE
