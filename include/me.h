@@ -93,15 +93,19 @@ const char* me_version(void);
  * identical on every path.
  *   ME_PATH_AUTO: SSD with 16x16 and 8x8 blocks on the matrix cores (i8 MFMA),
  *     everything else on the VALU kernels.  16x16 SSD with S <= 64 runs the
- *     band-walk kernel: each 16-row band's S2 term formed once in LDS for
+ *     band-walk kernel (each 16-row band's S2 term formed once in LDS for
  *     every block row in flight, no context scratch, ~1.1x the algorithmic
- *     HBM bytes; larger ranges the prepass + block-major pair.
+ *     HBM bytes: DESIGN.md) when a launch's strips of block columns fill the
+ *     GPU's CUs by themselves (e.g. 16 1080p frames per batched call);
+ *     otherwise (single frames, small batches, larger ranges) the prepass +
+ *     block-major pair.
  *   ME_PATH_VALU: VALU kernels only.
  *   ME_PATH_MFMA_TILES: 16x16 SSD on the 4x4-block-tile MFMA kernel (the
  *     fallback for rows that are not 16-byte aligned).
- *   ME_PATH_MFMA_LEAN: 16x16 SSD with S <= 64 forms its S2 term per
- *     workgroup and band (me_mfma_bmv_kernel, the kernel that also takes a
- *     partial bottom block row on the AUTO path).
+ *   ME_PATH_MFMA_LEAN: 16x16 SSD with S <= 64 on the band-walk kernel for
+ *     every launch (single frames split into segments of block rows; no
+ *     context scratch); a partial bottom block row, or rows the band-walk
+ *     kernel cannot take, on the per-workgroup S2 kernel (me_mfma_bmv_kernel).
  *   ME_PATH_MFMA_PREPASS: 16x16 SSD on the S2 prepass + block-major kernel
  *     (5 bytes of context scratch per reference pixel per frame of a batch).
  * The environment variable ME_PATH=auto|valu|tiles|lean|prepass sets the

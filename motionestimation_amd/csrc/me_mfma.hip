@@ -1706,6 +1706,27 @@ static bool plan_mfma_ssd8(const SearchArgs& p, MfmaGeom* g);
 // the tile kernel remains for row pitches / cur pointers that are not 16-byte aligned.
 static bool bm_auto(const SearchArgs& p) { return p.range <= 192; }
 
+// The automatic path's choice for `jobs` frames of p's shape per launch:
+// the band-walk kernel (lean: no prepass planes, ~1.1x the algorithmic HBM
+// bytes) when the launch's strips fill the CUs without splitting block rows
+// into segments (each segment re-forms 2 ceil(S/16) bands around it; a single
+// 1080p frame would be 8 segments of 9 rows: 68.8 us against 36.7 on the
+// prepass pair, 16 frames per launch 24.5 against 24.4: profiles/r05za_*).
+// ME_PATH_MFMA_LEAN (force) takes the band-walk kernel whenever it applies.
+// g holds the block-major plan on entry and the band-walk plan on success.
+static bool use_bw(const SearchArgs& p, MfmaGeom* g, int jobs, bool force = false) {
+  if (!g->bm) return false;
+  MfmaGeom t = *g;
+  t.bmv = 0;
+  if (!plan_bw(p, &t, jobs) || (!force && t.bw_segs != 1)) return false;
+  *g = t;
+  g->bmv_r = 1;
+  g->scratch_bytes = 0;
+  g->rp = nullptr;
+  g->s2 = g->s2h = nullptr;
+  return true;
+}
+
 bool plan_mfma_ssd(const SearchArgs& p, MfmaGeom* g) {
   if (p.cost_kind != COST_SSD) return false;
   if (p.blk == 8) return plan_mfma_ssd8(p, g);
@@ -1798,15 +1819,11 @@ bool plan_mfma_ssd(const SearchArgs& p, MfmaGeom* g) {
   g->s2 = p.scratch ? reinterpret_cast<int*>(p.scratch + rp_alloc) : nullptr;
   g->s2h = p.scratch ? reinterpret_cast<int*>(p.scratch + rp_alloc + s2_plane) : nullptr;
   // Automatic path, S <= 64: the band-walk kernel (me_band.hip) for the
-  // full-height rows, me_mfma_bmv_kernel for a partial bottom row; neither
-  // needs scratch.  ME_PATH_MFMA_PREPASS keeps the prepass + block-major pair.
+  // full-height rows, me_mfma_bmv_kernel for a partial bottom row, neither
+  // with scratch, when the frame's strips fill the CUs by themselves
+  // (use_bw); ME_PATH_MFMA_PREPASS keeps the prepass + block-major pair.
   g->bw = 0;
-  if (g->bm && !g->bmv && kernel_path() == 0 && plan_bw(p, g, 1)) {
-    g->bmv_r = 1;
-    g->scratch_bytes = 0;
-    g->rp = nullptr;
-    g->s2 = g->s2h = nullptr;
-  }
+  if (kernel_path() == 0 || kernel_path() == 3) use_bw(p, g, 1, kernel_path() == 3);
   if (g->bmv) {  // no planes: the kernel reads the reference plane
     g->scratch_bytes = 0;
     g->rp = nullptr;
@@ -1992,6 +2009,8 @@ static int batch_jobs(const MfmaGeom& g, int n) {
 size_t mfma_batch_scratch(const SearchArgs& p, int n) {
   MfmaGeom g;
   if (!plan_mfma_ssd(p, &g) || g.bmv || g.bw) return 0;
+  if (n >= 2 && kernel_path() == 0 && tuning().mfma_batch != 0 && use_bw(p, &g, n < MAX_JOBS ? n : MAX_JOBS))
+    return 0;  // the batch runs on the band-walk kernel
   const int m = batch_jobs(g, n);
   return m ? (size_t)m * batch_stride(g) : g.scratch_bytes;
 }
@@ -2020,6 +2039,8 @@ bool launch_mfma_jobs(const SearchArgs& base, const SearchJob* jobs, int n, hipS
   // row loads), else the batch runs job by job, each planned on its own
   for (int i = 1; i < n; i++)
     if ((uintptr_t)jobs[i].ref % 4 || (uintptr_t)jobs[i].cur % (g.bm ? 16 : 4)) return false;
+  // a launch of several frames may fill the CUs where one frame does not
+  if (!g.bw && kernel_path() == 0) use_bw(p, &g, n < MAX_JOBS ? n : MAX_JOBS);
   const bool lean = g.bmv || g.bw;  // no prepass planes
   const size_t stride = lean ? 0 : batch_stride(g);
   int m = batch_jobs(g, n);

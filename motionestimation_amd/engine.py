@@ -46,11 +46,12 @@ def plan_stripes(width: int, height: int, blk: int, span: int, shards: int) -> l
 
 def set_kernel_path(path: str) -> None:
     """'auto': 16x16 and 8x8 SSD on the matrix cores (i8 MFMA; 16x16 with
-    S <= 64 on the band-walk kernel), the rest on the VALU kernels; 'valu':
+    S <= 64 on the band-walk kernel when a launch's strips fill the CUs, else
+    the prepass + block-major pair), the rest on the VALU kernels; 'valu':
     VALU kernels only; 'tiles': as 'auto' with 16x16 SSD on the 4x4-block-tile
-    MFMA kernel; 'lean': as 'auto' with 16x16 SSD (S <= 64) forming S2 per
-    workgroup (me_mfma_bmv_kernel); 'prepass': 16x16 SSD on the S2 prepass +
-    block-major pair.  Process-wide; results are identical."""
+    MFMA kernel; 'lean': 16x16 SSD (S <= 64) on the band-walk kernel for every
+    launch (no prepass planes, no scratch); 'prepass': 16x16 SSD on the S2
+    prepass + block-major pair.  Process-wide; results are identical."""
     codes = {"auto": _lib.ME_PATH_AUTO, "valu": _lib.ME_PATH_VALU, "tiles": _lib.ME_PATH_MFMA_TILES,
              "lean": _lib.ME_PATH_MFMA_LEAN, "prepass": _lib.ME_PATH_MFMA_PREPASS}
     if path not in codes:

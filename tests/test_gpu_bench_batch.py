@@ -7,8 +7,9 @@ on the same frames must equal
   * the oracle restatement run live, frame by frame (SAD), and
   * the committed per-frame pins (tests/golden/bench_pins.json: SAD from the
     oracle, SSD from the unmodified reference's ref_dump).
-The SSD leg (ssd_mfma: one prepass + one block-major matrix-core launch for
-the 16 frames) and the 4K stripe leg's batch are pinned the same way.
+The SSD leg (ssd_mfma: one band-walk matrix-core launch for the 16 frames,
+plus the lean kernel's launch for their partial bottom block rows) and the 4K
+stripe leg's batch are pinned the same way.
 """
 import hashlib
 import os
@@ -62,12 +63,16 @@ def test_headline_batch_1080p_sad_equals_oracle_every_frame(engine):
         assert _hash(mv, co, 1920, 1080, 16, "sad") == pins[f], f"frame {f} pin"
 
 
-@pytest.mark.parametrize("path", ["auto", "lean"])
-def test_ssd_leg_batch_1080p_equals_reference_every_frame(engine, path):
+@pytest.mark.parametrize("path,kernel", [("auto", "mfma_bandwalk"), ("lean", "mfma_bandwalk"),
+                                         ("prepass", "mfma_prepass")])
+def test_ssd_leg_batch_1080p_equals_reference_every_frame(engine, path, kernel):
+    """The benched SSD launch (16 1080p frames) runs the band-walk kernel on
+    the automatic path (its strips fill the CUs) and equals the reference."""
     import motionestimation_amd as me
     me.set_kernel_path(path)
     try:
         fields = _search(engine, _batch("1080p"), 16, 32, "ssd")
+        assert me.last_search_path() == kernel, (path, me.last_search_path())
     finally:
         me.set_kernel_path("auto")
     pins = bench.load_pins("1080p", 16, 32, "ssd")

@@ -297,16 +297,16 @@ def test_band_walk_segments_and_batches(engine, ssd_path, shape, span):
     other frames, against the oracle (partial bottom rows: 368 = 23 x 16,
     1080 = 67 x 16 + 8, handed to the lean kernel)."""
     import torch
-    if ssd_path != "auto":
-        pytest.skip("band-walk geometry: automatic path only")
+    if ssd_path != "lean":
+        pytest.skip("band-walk geometry: the lean path forces the band-walk kernel")
     h, w = shape
     rng = np.random.default_rng(h + span)
     pairs = [_pair(rng, h, w, dx=int(rng.integers(-5, 6)), dy=int(rng.integers(-5, 6))) for _ in range(6)]
     ref, cur = pairs[0]
     _check(engine, ref, cur, span, f"{h}x{w} S{span} single")
-    # the automatic path of a single frame is the band-walk kernel (round 5:
-    # a missing scratch check had sent it to the VALU kernels, correct but 3x
-    # slower)
+    # the lean path runs the band-walk kernel on a single frame too (round 5:
+    # a missing scratch check had sent band-walk searches to the VALU
+    # kernels, correct but 3x slower)
     engine.full_search(ref, cur, 16, span, "ssd")
     assert me.last_search_path() == "mfma_bandwalk", me.last_search_path()
     dev = torch.device("cuda", 0)
@@ -362,12 +362,13 @@ def test_band_walk_forced_segment_rows(tmp_path, seg):
     assert "segments ok" in r.stdout
 
 
-@pytest.mark.parametrize("path,want", [("auto", "mfma_bandwalk"), ("prepass", "mfma_prepass"),
-                                       ("lean", "mfma_lean"), ("tiles", "mfma_tiles"), ("valu", "valu")])
+@pytest.mark.parametrize("path,want", [("auto", "mfma_prepass"), ("prepass", "mfma_prepass"),
+                                       ("lean", "mfma_bandwalk"), ("tiles", "mfma_tiles"), ("valu", "valu")])
 def test_kernel_path_reported(engine, path, want):
     """me_last_search_path names the kernel family each me_set_kernel_path
-    value runs for a 16x16 +-32 SSD search (single frame); SAD runs the VALU
-    kernels on every path."""
+    value runs for a 16x16 +-32 SSD search of one small frame (on the
+    automatic path its strips cannot fill the CUs: the prepass pair); SAD runs
+    the VALU kernels on every path."""
     rng = np.random.default_rng(11)
     ref, cur = _pair(rng, 256, 320, dx=2, dy=-1)
     try:
