@@ -331,12 +331,17 @@ def single_frame(eng, ref_t, cur_t, blk, span, cost, nb, cands_frame, dev, steps
             "parity": par}
 
 
-def ssd_beside(eng, ref_t, cur_t, blk, span, nb, cands_frame, dev, steps, pins, ramp_ms):
+def ssd_beside(eng, ref_t, cur_t, blk, span, nb, cands_frame, dev, steps, pins, ramp_ms, config):
     """The reference's own cost (MSE = SSD / 256) on the step's resident frame
     pairs ([F, H, W] stacks): B = 16 SSD runs on the matrix cores (i8 MFMA), the
-    F frames in one batched call (one prepass and one block-major launch).
-    Reported beside `value`; `kernel_ms` is per frame.  The last timed batch's
-    fields are checked against the reference's own (pins) and single searches."""
+    F frames in one batched call (16 1080p frames: one band-walk launch plus
+    the lean kernel's launch for the partial bottom block rows).  Reported
+    beside `value`; `kernel_ms` is per frame.  roofline.traffic: PMC bytes per
+    launch of the dominant kernel from the committed profile of the same
+    batch (tools/profile_all.sh, `<config>_b16_s<S>_ssd_f<F>`), and per frame
+    over every kernel of the search beside the algorithmic bytes.  The last
+    timed batch's fields are checked against the reference's own (pins) and
+    single searches."""
     import torch
     F, h, w = ref_t.shape
     nby = (h + blk - 1) // blk
@@ -353,12 +358,19 @@ def ssd_beside(eng, ref_t, cur_t, blk, span, nb, cands_frame, dev, steps, pins, 
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / steps / F
     tops = 2.0 * exact_absdiffs(w, h, blk, span) / (ms / 1e3) / 1e12
+    import motionestimation_amd as me
+    kernel = me.last_search_path()
     par = verify_fields(eng, batch_fields(mv, co, F), ref_t, cur_t, w, h, blk, span, "ssd",
                         pins, dev)
+    traffic, traffic_search = load_traffic(f"{config}_b{blk}_s{span}_ssd_f{F}")
     return {"value": cands_frame / (ms / 1e3), "unit": "candidates/s", "kernel_ms": ms,
             "steps": steps, "frames_per_step": F, "cost": "ssd (reference MSE argmin, bit-exact)",
+            "kernel_path": kernel,
             "roofline": {"bound": "mfma", "achieved": tops, "peak": I8_PEAK_TOPS,
-                         "unit": "TFLOP/s", "frac": tops / I8_PEAK_TOPS},
+                         "unit": "TFLOP/s", "frac": tops / I8_PEAK_TOPS,
+                         "traffic": traffic,
+                         "traffic_per_frame": traffic_search / F if traffic_search else None,
+                         "algorithmic_bytes_per_frame": 2 * w * h + 8 * nb},
             "parity": par}
 
 
@@ -1103,7 +1115,7 @@ def main():
             and blk == 16 and not args.no_ssd):
         line["ssd_mfma"] = ssd_beside(eng, ref_t, cur_t, blk, span, nb, cands_frame, dev,
                                       min(args.steps, 20), load_pins(args.config, blk, span, "ssd"),
-                                      args.ramp_ms)
+                                      args.ramp_ms, args.config)
         legs["ssd_mfma"] = line["ssd_mfma"]["parity"]
     if (rank == 0 and world == 1 and mode == "frames" and args.config == "1080p"
             and args.cost == "sad" and not args.no_ssim):
