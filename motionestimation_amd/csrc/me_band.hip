@@ -113,10 +113,12 @@ __device__ __forceinline__ v4i ldv4(uint32_t a) {
   return *reinterpret_cast<lds_cv4i*>((uintptr_t)a);
 }
 
-// LDS layout (bytes): K windows | K P0 planes | crec (searchers) | keys | ctl
+// LDS layout (bytes): K windows | K P0 planes | crec (searchers) | staged cur
+// rows (searchers) | keys | ctl
 __host__ __device__ constexpr int bw_win(int lp) { return BW_WIN_ROWS * lp; }
 __host__ __device__ inline int bw_lds_bytes(int lp, int pp, int ns, int nsw) {
-  return BW_K * bw_win(lp) + BW_K * 16 * pp * 4 + nsw * 16 * BW_CREC + nsw * ns * 8 + (int)sizeof(BwCtl);
+  return BW_K * bw_win(lp) + BW_K * 16 * pp * 4 + nsw * 16 * BW_CREC + nsw * 256 + nsw * ns * 8 +
+         (int)sizeof(BwCtl);
 }
 
 // Bounded spin on an LDS word (the handshake's ordering argument says it
@@ -151,7 +153,8 @@ __global__ __launch_bounds__(64 * (NSW + PW), 4) void me_mfma_bw_kernel(SearchAr
   uint8_t* xw = smem;
   int* p0 = reinterpret_cast<int*>(xw + BW_K * WIN);
   uint8_t* crec_all = reinterpret_cast<uint8_t*>(p0 + BW_K * P0PLANE);
-  unsigned long long* keys = reinterpret_cast<unsigned long long*>(crec_all + NSW * 16 * BW_CREC);
+  uint8_t* stage_all = crec_all + NSW * 16 * BW_CREC;
+  unsigned long long* keys = reinterpret_cast<unsigned long long*>(stage_all + NSW * 256);
   BwCtl* ctl = reinterpret_cast<BwCtl*>(keys + NSW * NS);
 
   const int tid = (int)threadIdx.x, lane = tid & 63;
@@ -312,19 +315,31 @@ __global__ __launch_bounds__(64 * (NSW + PW), 4) void me_mfma_bw_kernel(SearchAr
   const int xlo = max(bx - S, 0), xhi = min(bx + S, W - 16);
   const int i0c = xlo >> 4, i1c = xhi >> 4;
   uint8_t* crec = crec_all + wave * 16 * BW_CREC;
-  const uint8_t* cur_lane = p.cur + (ptrdiff_t)(lane - p.cur_row0) * p.stride + 16 * (bc0 + col);
 
-  // The first row entering at band b (this column and class) is prefetched
-  // into pf0 a band ahead; further ones (frame top, segment starts) are
-  // loaded when they enter.
-  u32x4 pf0 = {0u, 0u, 0u, 0u};
+  // The first row entering at band b (this column and class) is prefetched a
+  // band ahead by LDS DMA into the wave's 256-byte stage (16 lanes x 16
+  // bytes: no VGPRs live across the band); further ones (frame top, segment
+  // starts) are loaded when they enter.
+  uint8_t* stage = stage_all + wave * 256;
+  const __amdgpu_buffer_rsrc_t rcur =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.cur, (short)0, p.cur_bytes, 0x00020000);
   int pe0 = 0, pe1 = 0;  // this class's entering rows: pe0, pe0 + WPC, ... < pe1
   auto fetch = [&](int b) {
     const int e0 = max(E(b), r0), e1 = min(E(b + 1), r1);
     pe0 = e0 + ((cls - (e0 - r0)) % WPC + WPC) % WPC;
     pe1 = e1;
     if (hascol && lane < 16 && pe0 < pe1)
-      pf0 = *reinterpret_cast<const u32x4*>(cur_lane + (ptrdiff_t)(16 * pe0) * p.stride);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rcur, (__attribute__((address_space(3))) void*)stage, 16,
+          (uint32_t)((16 * pe0 + lane - p.cur_row0) * p.stride + 16 * (bc0 + col)), 0, 0, 0);
+  };
+  auto staged = [&]() {  // the prefetched row (lanes 0..15)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    return *reinterpret_cast<const u32x4*>(stage + 16 * (lane & 15));
+  };
+  auto cur_row = [&](int br) {  // block row br's cur rows (lane < 16: row 16 br + lane), loaded now
+    return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+        rcur, (uint32_t)opaque((16 * br + (lane & 15) - p.cur_row0) * p.stride + 16 * (bc0 + col)), 0, 0));
   };
   // A fragments of an entering row: bytes o .. o + 15 of record row
   // 2 q + (h >> 1), o = 16 + 16 (h & 1) - m (me_mfma_bm16_kernel's layout);
@@ -400,7 +415,7 @@ __global__ __launch_bounds__(64 * (NSW + PW), 4) void me_mfma_bw_kernel(SearchAr
       const int out = (br - p.block_row_begin) * p.nbx + bc0 + col;
       store_mv(p.mv, out, kk);
       if (p.cost) p.cost[out] = (uint32_t)(kk >> 32);
-      *kp = ~0ull;
+      *kp = ((unsigned long long)(uint32_t)opaque(-1) << 32) | (uint32_t)opaque(-1);  // (no pinned -1 pair)
     }
   };
 
@@ -454,7 +469,7 @@ __global__ __launch_bounds__(64 * (NSW + PW), 4) void me_mfma_bw_kernel(SearchAr
     fetch(bfirst);
     if (!(ABL && (g.bw_abl & 4)))
       for (int br = pe0; br < pe1; br += WPC)
-        enter(br, br == pe0 ? pf0 : *reinterpret_cast<const u32x4*>(cur_lane + (ptrdiff_t)(16 * br) * p.stride));
+        enter(br, br == pe0 ? staged() : cur_row(br));
 #pragma unroll 1
     for (int b = bfirst; b <= blast; b++) {
       const int k = b % BW_K;
@@ -516,9 +531,12 @@ __global__ __launch_bounds__(64 * (NSW + PW), 4) void me_mfma_bw_kernel(SearchAr
 #pragma unroll
             for (int r = 0; r < 4; r++) P[r] = (uint32_t)pv[r];
             if constexpr (E) {
+              // (x opaque: hoisted out of the band loop, the masks pinned
+              // VGPRs and spilled)
+              const int x0 = opaque(16 * i + 4 * h);
 #pragma unroll
               for (int r = 0; r < 4; r++) {
-                const int x = 16 * i + 4 * h + r;
+                const int x = x0 + r;
                 P[r] |= (x < xlo || x > xhi) ? 0x80000000u : 0u;
               }
             }
@@ -580,7 +598,7 @@ __global__ __launch_bounds__(64 * (NSW + PW), 4) void me_mfma_bw_kernel(SearchAr
       BW_ACC(4);
       if (b + 1 <= blast && !(ABL && (g.bw_abl & 4)))
         for (int br = pe0; br < pe1; br += WPC)
-          enter(br, br == pe0 ? pf0 : *reinterpret_cast<const u32x4*>(cur_lane + (ptrdiff_t)(16 * br) * p.stride));
+          enter(br, br == pe0 ? staged() : cur_row(br));
       BW_ACC(1);
     }
   }
