@@ -6,7 +6,7 @@
 # runs, so each kernel's launches are the timed workload's own)
 set -e
 TAG=${1:-r01}
-C="--no-cpu --no-stream --no-4k --no-single"
+C="--no-cpu --no-stream --no-4k --no-single --no-ssim"
 bash tools/profile.sh ${TAG}_1080p_sad --steps 20 --warmup 3 $C --no-ssd > gpurun_out/prof1.txt 2>&1
 bash tools/profile.sh ${TAG}_1080p_ssd --steps 20 --warmup 3 $C --cost ssd > gpurun_out/prof2.txt 2>&1
 bash tools/profile.sh ${TAG}_4k_sad --steps 4 --warmup 1 $C --no-ssd --config 4k > gpurun_out/prof3.txt 2>&1
