@@ -120,6 +120,11 @@ __host__ __device__ inline int bw_lds_bytes(int lp, int pp, int ns, int nsw) {
   return BW_K * bw_win(lp) + BW_K * 16 * pp * 4 + nsw * 16 * BW_CREC + nsw * 256 + nsw * ns * 8 +
          (int)sizeof(BwCtl);
 }
+// the partial bottom row's extra LDS: its nhb S2 planes, the producers' row
+// records and keys
+__host__ __device__ inline int bw_lds_hb_bytes(int pp, int ns, int nhb) {
+  return nhb ? nhb * 16 * pp * 4 + BW_PW * (16 * BW_CREC + ns * 8) : 0;
+}
 
 // Bounded spin on an LDS word (the handshake's ordering argument says it
 // ends; the bound keeps a broken invariant from hanging the GPU: an expired
@@ -152,10 +157,12 @@ __global__ __launch_bounds__(64 * (NSW + PW), 4) void me_mfma_bw_kernel(SearchAr
   const int P0PLANE = 16 * PP;  // ints
   uint8_t* xw = smem;
   int* p0 = reinterpret_cast<int*>(xw + BW_K * WIN);
-  uint8_t* crec_all = reinterpret_cast<uint8_t*>(p0 + BW_K * P0PLANE);
-  uint8_t* stage_all = crec_all + NSW * 16 * BW_CREC;
+  // (the partial bottom row's S2 planes, g.bw_hb of them, follow the ring)
+  const int nwr = NSW + (g.bw_hb ? PW : 0);  // waves with row records and keys
+  uint8_t* crec_all = reinterpret_cast<uint8_t*>(p0 + (BW_K + g.bw_hb) * P0PLANE);
+  uint8_t* stage_all = crec_all + nwr * 16 * BW_CREC;
   unsigned long long* keys = reinterpret_cast<unsigned long long*>(stage_all + NSW * 256);
-  BwCtl* ctl = reinterpret_cast<BwCtl*>(keys + NSW * NS);
+  BwCtl* ctl = reinterpret_cast<BwCtl*>(keys + nwr * NS);
 
   const int tid = (int)threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -182,6 +189,15 @@ __global__ __launch_bounds__(64 * (NSW + PW), 4) void me_mfma_bw_kernel(SearchAr
   auto hi = [&](int br) { return min(16 * br + S, H - 16) >> 4; };  // last band of row br
   auto E = [&](int b) { return b <= 0 ? 0 : b + Sc; };              // first row with lo >= b
   const int bfirst = lo(r0), blast = hi(r1 - 1);
+  // A partial bottom block row (height hbh < 16) is searched here when the
+  // planner gave it S2 planes (g.bw_hb > 0): by the producers of the job's
+  // last segment, after their bands, over bands lo_h .. hbrow (its last
+  // candidate row is H - hbh = 16 hbrow), with an hbh-row S2 they form with
+  // those bands.
+  const bool hbk = g.bw_hb > 0 && g.hb_row >= 0 && r1 == g.row0 + g.nrows;
+  const int hbrow = hbk ? g.hb_row : -1, hbh = g.hb;
+  const int lo_h = hbk ? lo(hbrow) : 0;
+  const int blast_p = hbk ? max(blast, hbrow) : blast;  // the bands the producers form
   const int nact = WPC * ncol;  // searcher waves that walk the bands (a column each)
 
   // ================================ producers
@@ -287,6 +303,29 @@ __global__ __launch_bounds__(64 * (NSW + PW), 4) void me_mfma_bw_kernel(SearchAr
         V = h_acc(x0, x1, V);
         out_row(k, ((o - 16) >> 1) + 1);
       }
+    }
+  };
+  // The partial row's S2 over hbh rows for band m into plane BW_K + (m - lo_h):
+  // the same sliding sum with an hbh-row window over the band's window rows
+  // (XOR-ed by produce already: u = w ^ 0xFF); runtime steps, a few bands per
+  // job.
+  auto produce_hb = [&](int m) {
+    const int k = BW_K + (m - lo_h);
+    const uint32_t xa = (uint32_t)opaque((int)lds_addr(xw + (m % BW_K) * WIN)) + 4u * (uint32_t)pg;
+    auto rd = [&](int t, v4i acc) {
+      return h_acc(ld32(xa + (uint32_t)(t * LP)) ^ 0x80808080u, ld32(xa + (uint32_t)(t * LP + 4)) ^ 0x80808080u, acc);
+    };
+    const v4i z = {0, 0, 0, 0};
+    V = z;
+    R = z;
+#pragma unroll 1
+    for (int t = 0; t < hbh; t++) V = rd(t, V);
+    out_row(k, 0);
+#pragma unroll 1
+    for (int j = 1; j < 16; j++) {
+      R = rd(j - 1, R);
+      V = rd(j + hbh - 1, V);
+      out_row(k, j);
     }
   };
   auto produce = [&](int k) __attribute__((always_inline)) {
@@ -419,11 +458,109 @@ __global__ __launch_bounds__(64 * (NSW + PW), 4) void me_mfma_bw_kernel(SearchAr
     }
   };
 
+  // The partial bottom row, block column c of the strip (a producer wave, once
+  // its bands are formed): its A fragments from its hbh cur rows (rows below
+  // as c'' = 0: they add nothing to X or Cc), one MFMA slot, the keys on its
+  // hbh-row S2 planes, its best over the bands -> its record.
+  auto hb_search = [&](int c) {
+    const int bxc = 16 * (bc0 + c);
+    const int xl = max(bxc - S, 0), xh = min(bxc + S, W - 16);
+    const int ia = xl >> 4, ib = xh >> 4;
+    const u32x4 v = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+        rcur, (uint32_t)((16 * hbrow + (lane & 15) - p.cur_row0) * p.stride + bxc), 0, 0));
+    const u32x4 x = (lane & 15) < hbh ? v ^ 0x7F7F7F7Fu : u32x4{0u, 0u, 0u, 0u};
+    int part = 0;
+    if (lane < 16) {
+      const u32x4 z = {0u, 0u, 0u, 0u};
+      u32x4* rec = reinterpret_cast<u32x4*>(crec + lane * BW_CREC);
+      rec[0] = z;
+      rec[1] = x;
+      rec[2] = z;
+#pragma unroll
+      for (int e = 0; e < 4; e++) {
+        part = __builtin_amdgcn_sdot4((int)x[e], (int)x[e], part, false);
+        part = __builtin_amdgcn_sdot4((int)x[e], 0x02020202, part, false);
+      }
+    }
+    part += __builtin_amdgcn_update_dpp(0, part, 0x111, 0xF, 0xF, false);
+    part += __builtin_amdgcn_update_dpp(0, part, 0x112, 0xF, 0xF, false);
+    part += __builtin_amdgcn_update_dpp(0, part, 0x114, 0xF, 0xF, false);
+    part += __builtin_amdgcn_update_dpp(0, part, 0x118, 0xF, 0xF, false);
+    const int ccv = __builtin_amdgcn_readlane(part, 15);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const int o = 16 + 16 * (h & 1) - n, sh = o & 3;
+    const uint32_t lb = lds_addr(crec) + (uint32_t)((h >> 1) * BW_CREC + (o & ~3));
+    v4i Ah[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      uint32_t d[5];
+#pragma unroll
+      for (int e = 0; e < 5; e++) d[e] = ld32(lb + (uint32_t)(2 * q * BW_CREC + 4 * e));
+#pragma unroll
+      for (int e = 0; e < 4; e++) Ah[q][e] = (int)__builtin_amdgcn_alignbyte(d[e + 1], d[e], sh);
+    }
+    const int ylo = max(16 * hbrow - S, 0), yhi = H - hbh;
+    uint32_t best = ~0u;
+    int bbest = 0;
+#pragma unroll 1
+    for (int b = lo_h; b <= hbrow; b++) {
+      const int kw = b % BW_K;
+      if (!bw_wait(p, lane, [&] {
+            return __hip_atomic_load(&ctl->ready[kw], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == b;
+          }))
+        return false;
+      const uint32_t xb = lds_addr(xw + kw * WIN) + (uint32_t)((n + (h >> 1)) * LP + 16 * (h & 1) - 16 * tc0);
+      const uint32_t pb = lds_addr(p0 + (BW_K + b - lo_h) * P0PLANE) + (uint32_t)((n * PP + 4 * h - 16 * tc0) * 4);
+      uint32_t bc = ~0u;
+#pragma unroll 1
+      for (int i = ia; i <= ib; i++) {
+        v4i acc = {0, 0, 0, 0};
+#pragma unroll
+        for (int q = 0; q < 8; q++) acc = MFMA16(Ah[q], ldv4(xb + (uint32_t)(16 * i + 2 * q * LP)), acc, 0, 0, 0);
+        const v4i pv = ldv4(pb + (uint32_t)(64 * i));
+        uint32_t k[4];
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const int xx = 16 * i + 4 * h + r;
+          k[r] = ((uint32_t)acc[r] << 7) + ((uint32_t)pv[r] | ((xx < xl || xx > xh) ? 0x80000000u : 0u));
+        }
+        bc = umin3(umin3(bc, k[0], k[1]), k[2], k[3]);
+      }
+      const int y = 16 * b + n;
+      if (y >= ylo && y <= yhi && (bc >> 6) < (best >> 6)) {
+        best = bc;
+        bbest = b;
+      }
+    }
+    // best over the lanes -> the block's record (as emit)
+    unsigned long long* kp = keys + wave * NS;
+    const uint32_t hk = best >> 6;
+    if (hk < (1u << 25)) {
+      const uint32_t cost = hk - 1u - (1u << 23) + (uint32_t)ccv;
+      const int idx = (int)(best & 63u);
+      const int dx = 16 * (tc0 + (idx >> 2)) + 4 * h + (idx & 3) - bxc;
+      const int dy = 16 * bbest + n - 16 * hbrow;
+      const unsigned long long key = ((unsigned long long)cost << 32) |
+                                     ((uint32_t)(dy + 32768) << 16) | (uint32_t)(dx + 32768);
+      asm volatile("ds_min_u64 %0, %1" : : "v"(lds_addr(kp)), "v"(key) : "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane == 0) {
+      const unsigned long long kk = *kp;
+      const int out = (hbrow - p.block_row_begin) * p.nbx + bc0 + c;
+      store_mv(p.mv, out, kk);
+      if (p.cost) p.cost[out] = (uint32_t)(kk >> 32);
+      *kp = ~0ull;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    return true;
+  };
+
 #ifdef ME_STAMPS
   unsigned long long bw_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
   BW_T0();
-  if (tid < NSW * NS) keys[tid] = ~0ull;
+  if (tid < nwr * NS) keys[tid] = ~0ull;
   if (tid < BW_K) {
     ctl->ready[tid] = -(1 << 30);
     ctl->done[tid] = 0;
@@ -448,11 +585,11 @@ __global__ __launch_bounds__(64 * (NSW + PW), 4) void me_mfma_bw_kernel(SearchAr
       dma_win(m, k);
       return true;
     };
-    bool ok = bfirst + pw > blast || claim(bfirst + pw);
+    bool ok = bfirst + pw > blast_p || claim(bfirst + pw);
 #pragma unroll 1
-    for (int m = bfirst + pw; ok && m <= blast; m += PW) {
+    for (int m = bfirst + pw; ok && m <= blast_p; m += PW) {
       const int k = m % BW_K;
-      const bool next = m + PW <= blast;
+      const bool next = m + PW <= blast_p;
       if (next) ok = claim(m + PW);
       BW_ACC(1);
       // band m's window landed (band m + PW's DMA may still be in flight)
@@ -460,11 +597,17 @@ __global__ __launch_bounds__(64 * (NSW + PW), 4) void me_mfma_bw_kernel(SearchAr
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DMA_N) : "memory");
       else
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (!(ABL && (g.bw_abl & 1))) produce(k);
+      if (!(ABL && (g.bw_abl & 1))) {
+        produce(k);
+        if (hbk && m >= lo_h) produce_hb(m);
+      }
       BW_ACC(5);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the window and P0 stores landed
       if (lane == 0) __hip_atomic_store(&ctl->ready[k], m, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
+    // then the partial bottom row: producer pw takes columns pw, pw + PW, ...
+#pragma unroll 1
+    for (int c = pw; ok && hbk && c < ncol; c += PW) ok = hb_search(c);
   } else if (hascol) {
     fetch(bfirst);
     if (!(ABL && (g.bw_abl & 4)))
@@ -686,6 +829,19 @@ bool plan_bw(const SearchArgs& p, MfmaGeom* g, int jobs) {
   g->bw_segs = (rows + best_l - 1) / best_l;
   g->lds = bw_lds_bytes(lp, pp, ns, nsw);
   if (g->lds > 160 * 1024 / wgs_cu) return false;
+  // A partial bottom block row (rows H - hb .. H - 1) joins the walk when its
+  // hb-row S2 planes fit in LDS beside the ring: one per band it meets, bands
+  // lo .. hb_row (its last candidate row is H - hb = 16 hb_row); otherwise it
+  // is a second launch of the lean kernel (launch_bw_jobs).
+  g->bw_hb = 0;
+  if (g->hb_row >= 0 && tuning().bw_hb != 0) {
+    const int nhb = g->hb_row - (std::max(16 * g->hb_row - S, 0) >> 4) + 1;
+    const int lds_hb = g->lds + bw_lds_hb_bytes(pp, ns, nhb);
+    if (lds_hb <= 160 * 1024 / wgs_cu) {
+      g->bw_hb = nhb;
+      g->lds = lds_hb;
+    }
+  }
   g->bw = 1;
   return true;
 }

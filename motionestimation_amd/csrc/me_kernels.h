@@ -181,6 +181,7 @@ struct MfmaGeom {
   int bw_segs;           // segments per job
   int bw_lp, bw_pp;      // window row pitch (bytes), P0 plane row pitch (ints)
   int bw_abl;            // tuning build only: ablation bits (ME_BW_ABL), 0 in the product
+  int bw_hb;             // S2 planes of a partial bottom row run by the band-walk kernel (0: by bmv)
 };
 size_t mfma_merge_tiles(const SearchArgs& p);  // tiles the merge buffers must cover
 bool plan_mfma_ssd(const SearchArgs& p, MfmaGeom* g);

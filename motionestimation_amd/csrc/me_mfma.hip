@@ -1942,7 +1942,7 @@ static hipError_t launch_bmv(const SearchArgs& p, const MfmaGeom& g, const MfmaJ
 static hipError_t launch_bw_jobs(const SearchArgs& p, const MfmaGeom& g, const MfmaJobs& jb,
                                  hipStream_t stream) {
   hipError_t e = launch_bw(p, g, jb, stream);
-  if (e != hipSuccess || g.hb_row < 0) return e;
+  if (e != hipSuccess || g.hb_row < 0 || g.bw_hb > 0) return e;  // (bw_hb: the row ran in the walk)
   MfmaGeom t = g;
   t.bw = 0;
   t.bmv = 1;
