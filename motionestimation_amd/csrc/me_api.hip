@@ -80,6 +80,7 @@ static Tuning read_tuning() {
   env_int("ME_BW", 0, 1, &t.bw);
   env_int("ME_BW_SEG", 1, 4096, &t.bw_seg);
   env_int("ME_BW_HB", 0, 1, &t.bw_hb);
+  env_int("ME_BW_XT", 0, 1, &t.bw_xt);
   env_int("ME_BW_ABL", 0, 1023, &t.bw_abl);
   if (const char* e = getenv("ME_FAIR_T")) {
     int lo = 0, hi = 0;

@@ -148,6 +148,47 @@ __device__ __forceinline__ bool bw_wait(const SearchArgs& p, int lane, Pred ok) 
 // slots, each published by its producer and released by its searchers, so a
 // wave's band-end work and its waits overlap the MFMAs of the SIMD's other
 // waves instead of every wave meeting at a barrier each band.
+// Workgroup -> (strip item, segment).  Items u = job * strips + strip.
+// Uniform (bw_xt = 0): XCD-banded workgroup index, segment-major in a job.
+// Per-XCD tail split (bw_xt = 1): XCD x = blockIdx & 7 owns a contiguous run
+// of the items (neighbouring strips share window rows in its L2) and walks
+// them whole, one per CU per round; the last partial round's kx items
+// (kx = items mod CUs per XCD) are cut into st segments each so that round
+// fills the XCD's CUs too (a whole strip item takes rows + 2 ceil(S/16) + 2
+// band times; its st segments ~ rows / st + that).  Launch order within an
+// XCD is blockIdx order, so the segments run last.
+struct BwItem {
+  int u, seg, rows;
+};
+__host__ __device__ inline void bw_xcd_split(int nx, int cx, int rows, int* main, int* kx, int* st,
+                                             int* L) {
+  int k = nx % cx, s = 1;
+  if (k) s = max(1, min(cx / k, rows / 4));
+  const int l = (rows + s - 1) / s;
+  *kx = k;
+  *L = l;
+  *st = (rows + l - 1) / l;
+  *main = nx - k;
+}
+__device__ __forceinline__ BwItem bw_item(const MfmaGeom& g, int jobs) {
+  if (!g.bw_xt) {
+    int lin = mfma::xcd_banded_index();
+    const int per = g.bw_strips * g.bw_segs, j = lin / per;
+    lin -= j * per;
+    const int seg = lin / g.bw_strips;
+    return {j * g.bw_strips + lin - seg * g.bw_strips, seg, g.bw_seg_rows};
+  }
+  const int b = (int)blockIdx.x, x = b & 7, m = b >> 3;
+  const int U = jobs * g.bw_strips, q = U >> 3, rem = U & 7;
+  const int nx = q + (x < rem ? 1 : 0), u0 = x * q + min(x, rem);
+  int mainx, kx, st, L;
+  bw_xcd_split(nx, g.bw_cx, g.bw_seg_rows, &mainx, &kx, &st, &L);
+  if (m < mainx) return {u0 + m, 0, g.bw_seg_rows};
+  const int t = m - mainx;
+  if (t >= kx * st) return {-1, 0, 0};
+  return {u0 + mainx + t % kx, t / kx, L};
+}
+
 template <int C, int NS, int LP, int NSW, int PW, bool ABL>
 __global__ __launch_bounds__(64 * (NSW + PW), 4) void me_mfma_bw_kernel(SearchArgs p, MfmaGeom g, MfmaJobs jb) {
   constexpr int WPC = NSW / C;  // row classes per column
@@ -171,15 +212,16 @@ __global__ __launch_bounds__(64 * (NSW + PW), 4) void me_mfma_bw_kernel(SearchAr
   const int pw = wave - NSW;                 // producers: index
   const int n = lane & 15, h = lane >> 4;
   const int S = p.range, W = p.width, H = p.height;
-  int lin = mfma::xcd_banded_index();
-  {  // batched launch: jobs are consecutive runs of jb.wgs workgroups
-    const int j = lin / jb.wgs;
-    lin -= j * jb.wgs;
+  int strip, r0, r1;
+  {
+    const BwItem it = bw_item(g, jb.n);
+    if (it.u < 0) return;  // a slot past its XCD's items (whole workgroup)
+    const int j = it.u / g.bw_strips;
+    strip = it.u - j * g.bw_strips;
     mfma_job(jb, j, p, g);
+    r0 = g.row0 + it.seg * it.rows;
+    r1 = min(r0 + it.rows, g.row0 + g.nrows);
   }
-  const int seg = lin / g.bw_strips, strip = lin - seg * g.bw_strips;
-  const int r0 = g.row0 + seg * g.bw_seg_rows;
-  const int r1 = min(r0 + g.bw_seg_rows, g.row0 + g.nrows);
   const int bc0 = strip * C, ncol = min(C, g.nbx - bc0);
   const int tc0 = max(16 * bc0 - S, 0) >> 4;  // first tile column of the strip window
   const int tcl = min(16 * (bc0 + ncol - 1) + S, W - 16) >> 4;
@@ -827,6 +869,14 @@ bool plan_bw(const SearchArgs& p, MfmaGeom* g, int jobs) {
   g->bw_seg_rows = best_l;
   g->bw_abl = tuning().bw_abl;
   g->bw_segs = (rows + best_l - 1) / best_l;
+  // Launches of whole rounds of strips take the per-XCD tail split instead.
+  g->bw_xt = 0;
+  g->bw_cx = bw_cu_count() / 8;
+  if (tuning().bw_xt != 0 && tuning().bw_seg == 0 && per >= cus && g->bw_cx > 0) {
+    g->bw_xt = 1;
+    g->bw_seg_rows = rows;
+    g->bw_segs = 1;
+  }
   g->lds = bw_lds_bytes(lp, pp, ns, nsw);
   if (g->lds > 160 * 1024 / wgs_cu) return false;
   // A partial bottom block row (rows H - hb .. H - 1) joins the walk when its
@@ -851,7 +901,18 @@ hipError_t launch_bw(const SearchArgs& p, const MfmaGeom& g0, const MfmaJobs& jb
   g.nrows = g0.nrows - (g0.hb_row >= 0 ? 1 : 0);  // full-height rows: the kernel's
   MfmaJobs jb = jb0;
   jb.wgs = g.bw_strips * g.bw_segs;
-  const dim3 grid((unsigned)(jb.n * jb.wgs)), blk(64 * (g.bw_nsw + g.bw_pw));
+  long wgs = (long)jb.n * jb.wgs;
+  if (g.bw_xt) {  // 8 XCDs x the most slots one of them needs (bw_item)
+    const long per = (long)jb.n * g.bw_strips;
+    int wmax = 0;
+    for (int nx : {(int)(per / 8), (int)((per + 7) / 8)}) {
+      int mainx, kx, st, L;
+      bw_xcd_split(nx, g.bw_cx, g.bw_seg_rows, &mainx, &kx, &st, &L);
+      wmax = std::max(wmax, mainx + kx * st);
+    }
+    wgs = 8L * wmax;
+  }
+  const dim3 grid((unsigned)wgs), blk(64 * (g.bw_nsw + g.bw_pw));
   hipError_t e;
   // ablation instances (tuning build only: ME_BW_ABL) are separate kernels
 #define ME_BW_CASE(C, NS, LP, NSW, PW)                                                          \

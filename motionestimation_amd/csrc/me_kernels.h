@@ -179,6 +179,8 @@ struct MfmaGeom {
   int bw_strips;         // strips per job
   int bw_seg_rows;       // block rows per workgroup
   int bw_segs;           // segments per job
+  int bw_xt;             // per-XCD tail split (bw_cx CUs per XCD): workgroup decode in bw_item()
+  int bw_cx;
   int bw_lp, bw_pp;      // window row pitch (bytes), P0 plane row pitch (ints)
   int bw_abl;            // tuning build only: ablation bits (ME_BW_ABL), 0 in the product
   int bw_hb;             // S2 planes of a partial bottom row run by the band-walk kernel (0: by bmv)

@@ -325,6 +325,36 @@ def test_band_walk_segments_and_batches(engine, ssd_path, shape, span):
         np.testing.assert_array_equal(co[f], oc, err_msg=f"frame {f}")
 
 
+@pytest.mark.parametrize("shape,span,frames", [((368, 656), 64, 16), ((360, 640), 32, 32)])
+def test_band_walk_xcd_tail_split(engine, ssd_path, shape, span, frames):
+    """Batches whose strips fill whole rounds of CUs walk them whole and cut
+    each XCD's last partial round into segments (bw_item in me_band.hip):
+    368 x 656 S64, 16 frames = 336 strips (42 per XCD: 10 tail strips in 3
+    segments each); 360 x 640 S32, 32 frames = 320 strips (8 tail strips in 4
+    segments, with the partial bottom row 360 = 22 x 16 + 8)."""
+    import torch
+    if ssd_path == "prepass":
+        pytest.skip("band-walk geometry")
+    h, w = shape
+    rng = np.random.default_rng(7 * h + span)
+    pairs = [_pair(rng, h, w, dx=int(rng.integers(-6, 7)), dy=int(rng.integers(-6, 7))) for _ in range(frames)]
+    dev = torch.device("cuda", 0)
+    nb = me.num_blocks(w, h, 16)
+    rt = torch.from_numpy(np.stack([r for r, _ in pairs])).to(dev)
+    ct = torch.from_numpy(np.stack([c for _, c in pairs])).to(dev)
+    mv = torch.empty((frames * nb, 2), dtype=torch.int16, device=dev)
+    co = torch.empty(frames * nb, dtype=torch.int32, device=dev)
+    engine.search_batch_device(rt, 0, ct, 0, w, h, 16, span, "ssd", 0, (h + 15) // 16, mv, co)
+    torch.cuda.synchronize()
+    engine.device_check()
+    assert me.last_search_path() == "mfma_bandwalk", me.last_search_path()
+    mv, co = mv.cpu().numpy().reshape(frames, nb, 2), co.cpu().numpy().view(np.uint32).reshape(frames, nb)
+    for f, (r, c) in enumerate(pairs):
+        omv, oc, _ = O.full_search(r, c, 16, span, "ssd", threads=NT)
+        np.testing.assert_array_equal(mv[f], omv, err_msg=f"frame {f}")
+        np.testing.assert_array_equal(co[f], oc, err_msg=f"frame {f}")
+
+
 _SEG_SCRIPT = r"""
 import sys
 sys.path.insert(0, {repo!r}); sys.path.insert(0, {tests!r})
