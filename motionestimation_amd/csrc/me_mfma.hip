@@ -212,16 +212,33 @@ __device__ __forceinline__ void prep_tile(const SearchArgs& p, const MfmaGeom& g
 
 template <int B>
 __global__ __launch_bounds__(PREP_T) void me_ssd_prep_kernel(SearchArgs p, MfmaGeom g, MfmaJobs jb) {
-  mfma_job(jb, (int)blockIdx.z, p, g);  // z: the job of a batched launch
+  // Tiles (tx, ty, job) in XCD bands: XCD k (dispatch order, bid % 8) takes
+  // the k-th eighth of the row-major tile order, so the 128-byte lines two
+  // neighbouring tiles share (a tile reads 80 columns) and the 7 halo rows
+  // between tile rows are fetched into one L2 (round-robin tiles over the
+  // XCDs fetched each line into two or three: 3x the plane's bytes).
+  int bx, by, bz;
+  {
+    const int gx = (int)gridDim.x, gxy = gx * (int)gridDim.y;
+    const int nwg = gxy * (int)gridDim.z;
+    const int bid = (int)blockIdx.x + gx * ((int)blockIdx.y + (int)gridDim.y * (int)blockIdx.z);
+    const int x = bid & 7, m = bid >> 3, q = nwg >> 3, rem = nwg & 7;
+    const int lin = x * q + min(x, rem) + m;
+    bz = lin / gxy;
+    by = (lin - bz * gxy) / gx;
+    bx = lin - bz * gxy - by * gx;
+  }
+  mfma_job(jb, bz, p, g);  // z: the job of a batched launch
   __shared__ __align__(16) int vs[64 * VS_P];
   __shared__ __align__(16) uint8_t rpt[64 * RPT_P];
-  // blockIdx.y < nmain: rp and s2 rows [64 y, +64); past it: s2h rows from s2h_row0
+  // by < nmain: rp and s2 rows [64 by, +64); past it: s2h rows from s2h_row0
+  // (B = 8: no rp plane, the search kernel stages the reference itself)
   const int nmain = (g.rows_alloc + 63) / 64;
-  const bool hpass = (int)blockIdx.y >= nmain;
-  const int x0 = (int)blockIdx.x * 64;
+  const bool hpass = by >= nmain;
+  const int x0 = bx * 64;
   PS_STAMP(0);
   if (hpass) {  // hb-row sums for the partial bottom block row's lanes
-    const int r0 = g.s2h_row0 + 64 * ((int)blockIdx.y - nmain);
+    const int r0 = g.s2h_row0 + 64 * (by - nmain);
     switch (g.hb) {
 #define ME_HB(k) case k: if constexpr (k < B) prep_tile<k, B>(p, g, vs, rpt, g.s2h, x0, r0, g.s2h_row0, false); break;
       ME_HB(1) ME_HB(2) ME_HB(3) ME_HB(4) ME_HB(5) ME_HB(6) ME_HB(7) ME_HB(8)
@@ -231,7 +248,7 @@ __global__ __launch_bounds__(PREP_T) void me_ssd_prep_kernel(SearchArgs p, MfmaG
     }
     return;
   }
-  prep_tile<B, B>(p, g, vs, rpt, g.s2, x0, 64 * (int)blockIdx.y, 0, true);
+  prep_tile<B, B>(p, g, vs, rpt, g.s2, x0, 64 * by, 0, B == 16);
   PS_STAMP(3);
 }
 
@@ -675,16 +692,21 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd8_kernel(SearchArgs p, M
   int gx = 0;                 // the group being searched
   int X0 = xa & ~3;           // its window column origin
 
-  const __amdgpu_buffer_rsrc_t rrp =
-      __builtin_amdgcn_make_buffer_rsrc((void*)g.rp, (short)0, g.rp_bytes, 0x00020000);
+  // The window straight from the reference plane into copy 0 (rows past the
+  // resident ones read as 0 through the buffer range; bytes past W belong to
+  // masked candidates only); the copy pass turns it into r ^ 0x80 in place and
+  // writes the shifted copies.  (A separate raw-row region cost the fifth
+  // workgroup per CU -- 35 KB -- and 3 % at 8K; prefetching it did not help.)
+  const __amdgpu_buffer_rsrc_t rref =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.ref, (short)0, p.ref_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rs2 =
       __builtin_amdgcn_make_buffer_rsrc((void*)g.s2, (short)0, g.s2_bytes, 0x00020000);
 
   auto stage = [&](int y0) {
-    const int base = (y0 - g.ya0) * g.pitch + X0;
-    dma16(rrp, smem, COPY, [&](int d) {
+    const int base = (y0 - p.ref_row0) * p.stride + X0;
+    dma16(rref, smem, COPY, [&](int d) {
       const int rho = d / WP, k = d - rho * WP;
-      return (uint32_t)(base + rho * g.pitch + k);
+      return (uint32_t)(base + rho * p.stride + k);
     });
     const int sbase = ((y0 - g.ya0) * g.pitch + xa + 64 * gx) * 4;
     dma16(rs2, s2t, L * RB, [&](int d) {
@@ -698,17 +720,35 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd8_kernel(SearchArgs p, M
     typedef __attribute__((address_space(3))) u32x4 lds_w128;
     constexpr int QW = WP / 16;
     const uint32_t lbase = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) uint8_t*)smem);
-    for (int i = opaque(tid); i < CROWS * QW; i += 256) {
-      const int rho = i / QW, c = i - rho * QW;
+    // every thread reads its (at most 2) 16-byte granules and the word after
+    // each before anyone overwrites copy 0
+    constexpr int NI = (CROWS * QW + 255) / 256;
+    u32x4 w[NI];
+    uint32_t nx[NI];
+    const int t0 = opaque(tid);
+#pragma unroll
+    for (int k = 0; k < NI; k++) {
+      const int i = t0 + 256 * k, rho = i / QW, c = i - rho * QW;
       const uint32_t off = (uint32_t)(rho * WP + 16 * c);
-      const u32x4 w = *reinterpret_cast<lds_w128*>((uintptr_t)(lbase + off));
-      const uint32_t nx = c + 1 < QW ? *reinterpret_cast<lds_w32*>((uintptr_t)(lbase + off + 16)) : 0u;
-      sfor<1, 4>([&](auto SG) {
-        constexpr int sg = decltype(SG)::value;
-        const u32x4 o = {__builtin_amdgcn_alignbyte(w[1], w[0], sg), __builtin_amdgcn_alignbyte(w[2], w[1], sg),
-                         __builtin_amdgcn_alignbyte(w[3], w[2], sg), __builtin_amdgcn_alignbyte(nx, w[3], sg)};
-        *reinterpret_cast<lds_w128*>((uintptr_t)(lbase + sg * COPY + off)) = o;
-      });
+      if (i < CROWS * QW) {
+        w[k] = *reinterpret_cast<lds_w128*>((uintptr_t)(lbase + off)) ^ 0x80808080u;
+        nx[k] = c + 1 < QW ? *reinterpret_cast<lds_w32*>((uintptr_t)(lbase + off + 16)) ^ 0x80808080u : 0u;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NI; k++) {
+      const int i = t0 + 256 * k, rho = i / QW, c = i - rho * QW;
+      const uint32_t off = (uint32_t)(rho * WP + 16 * c);
+      if (i < CROWS * QW) {
+        *reinterpret_cast<lds_w128*>((uintptr_t)(lbase + off)) = w[k];
+        sfor<1, 4>([&](auto SG) {
+          constexpr int sg = decltype(SG)::value;
+          const u32x4 o = {__builtin_amdgcn_alignbyte(w[k][1], w[k][0], sg), __builtin_amdgcn_alignbyte(w[k][2], w[k][1], sg),
+                           __builtin_amdgcn_alignbyte(w[k][3], w[k][2], sg), __builtin_amdgcn_alignbyte(nx[k], w[k][3], sg)};
+          *reinterpret_cast<lds_w128*>((uintptr_t)(lbase + sg * COPY + off)) = o;
+        });
+      }
     }
   };
 
@@ -1861,23 +1901,23 @@ static bool plan_mfma_ssd8(const SearchArgs& p, MfmaGeom* g) {
   g->ngxw = g->ngx;  // one workgroup walks all of a tile's groups
   g->km = ME_SSD8_KM;  // L = 16 km candidate rows per chunk
   const int L = 16 * g->km;
-  g->lds = 4 * (L + 8) * ME_SSD8_WP + 16 * 8 + 16 * 4 + (L + 1) * 256;
+  g->lds = 4 * (L + 8) * ME_SSD8_WP + 16 * 8 + 16 * 4 + (L + 1) * 256;  // 30.7 KB: 5 workgroups per CU
   g->ya0 = max(r0 * 8 - S, 0);
   const int ya1 = min(r1 * 8 + S, H);
   g->rp_rows = ya1 - g->ya0;
   g->pitch = (W + 15) & ~15;
   g->rows_alloc = g->rp_rows + 80;
   g->s2h_row0 = 0;
+  // S2 plane only: the kernel stages the reference rows itself (no r ^ 0x80 plane)
   const size_t plane = (size_t)g->rows_alloc * g->pitch;
-  const size_t rp_alloc = (plane + 255) & ~(size_t)255;
   const size_t s2_plane = plane * 4;
-  if (rp_alloc + s2_plane >= (1ull << 31)) return false;
-  g->rp_bytes = (uint32_t)plane;
+  if (s2_plane >= (1ull << 31)) return false;
+  g->rp_bytes = 0;
   g->s2_bytes = (uint32_t)s2_plane;
   g->s2h_off = 0;
-  g->scratch_bytes = rp_alloc + s2_plane;
-  g->rp = reinterpret_cast<int8_t*>(p.scratch);
-  g->s2 = p.scratch ? reinterpret_cast<int*>(p.scratch + rp_alloc) : nullptr;
+  g->scratch_bytes = s2_plane;
+  g->rp = nullptr;
+  g->s2 = p.scratch ? reinterpret_cast<int*>(p.scratch) : nullptr;
   g->s2h = nullptr;
   g->mkeys = p.mkeys;
   g->mcnt = p.mcnt;
