@@ -659,6 +659,8 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd8_kernel(SearchArgs p, M
   unsigned long long* keys = reinterpret_cast<unsigned long long*>(smem + 4 * COPY);
   int* cc = reinterpret_cast<int*>(smem + 4 * COPY + 16 * 8);
   uint8_t* s2t = smem + 4 * COPY + 16 * 8 + 16 * 4;  // [L][64] ints
+  constexpr int QW = WP / 16;                        // 16-byte granules per copy row
+  uint8_t* nxt = s2t + (L + 1) * RB;                 // [CROWS][QW] words: the 4 bytes after each granule
 
   const int tid = (int)threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n = lane & 15, h = lane >> 4;
@@ -708,6 +710,19 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd8_kernel(SearchArgs p, M
       const int rho = d / WP, k = d - rho * WP;
       return (uint32_t)(base + rho * p.stride + k);
     });
+    // and the word after every granule, apart: the copy pass then reads no
+    // byte it (or another thread) overwrites, so it needs no barrier between
+    // its reads and its writes
+    {
+      const int t = opaque(tid), ln = t & 63, wv = t >> 6;
+      for (int s0 = 64 * wv; s0 < CROWS * QW; s0 += 256) {
+        const int d = s0 + ln, rho = d / QW, c = d - rho * QW;
+        if (d < CROWS * QW)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(
+              rref, (__attribute__((address_space(3))) void*)(nxt + 4 * s0), 4,
+              (uint32_t)(base + rho * p.stride + 16 * (c + 1)), 0, 0, 0);
+      }
+    }
     const int sbase = ((y0 - g.ya0) * g.pitch + xa + 64 * gx) * 4;
     dma16(rs2, s2t, L * RB, [&](int d) {
       const int rho = d / RB, k = d - rho * RB;
@@ -718,37 +733,23 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd8_kernel(SearchArgs p, M
     typedef __attribute__((address_space(3))) uint32_t lds_w32;
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     typedef __attribute__((address_space(3))) u32x4 lds_w128;
-    constexpr int QW = WP / 16;
     const uint32_t lbase = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) uint8_t*)smem);
-    // every thread reads its (at most 2) 16-byte granules and the word after
-    // each before anyone overwrites copy 0
-    constexpr int NI = (CROWS * QW + 255) / 256;
-    u32x4 w[NI];
-    uint32_t nx[NI];
-    const int t0 = opaque(tid);
-#pragma unroll
-    for (int k = 0; k < NI; k++) {
-      const int i = t0 + 256 * k, rho = i / QW, c = i - rho * QW;
+    const uint32_t nbase = lbase + (uint32_t)(nxt - smem);
+    // a thread's granule of copy 0 is read and rewritten by that thread only;
+    // the word after it comes from the nxt table (the granule's last shifted
+    // bytes beyond the 71 the lanes read are don't-cares)
+    for (int i = opaque(tid); i < CROWS * QW; i += 256) {
+      const int rho = i / QW, c = i - rho * QW;
       const uint32_t off = (uint32_t)(rho * WP + 16 * c);
-      if (i < CROWS * QW) {
-        w[k] = *reinterpret_cast<lds_w128*>((uintptr_t)(lbase + off)) ^ 0x80808080u;
-        nx[k] = c + 1 < QW ? *reinterpret_cast<lds_w32*>((uintptr_t)(lbase + off + 16)) ^ 0x80808080u : 0u;
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < NI; k++) {
-      const int i = t0 + 256 * k, rho = i / QW, c = i - rho * QW;
-      const uint32_t off = (uint32_t)(rho * WP + 16 * c);
-      if (i < CROWS * QW) {
-        *reinterpret_cast<lds_w128*>((uintptr_t)(lbase + off)) = w[k];
-        sfor<1, 4>([&](auto SG) {
-          constexpr int sg = decltype(SG)::value;
-          const u32x4 o = {__builtin_amdgcn_alignbyte(w[k][1], w[k][0], sg), __builtin_amdgcn_alignbyte(w[k][2], w[k][1], sg),
-                           __builtin_amdgcn_alignbyte(w[k][3], w[k][2], sg), __builtin_amdgcn_alignbyte(nx[k], w[k][3], sg)};
-          *reinterpret_cast<lds_w128*>((uintptr_t)(lbase + sg * COPY + off)) = o;
-        });
-      }
+      const u32x4 w = *reinterpret_cast<lds_w128*>((uintptr_t)(lbase + off)) ^ 0x80808080u;
+      const uint32_t nx = *reinterpret_cast<lds_w32*>((uintptr_t)(nbase + 4u * (uint32_t)i)) ^ 0x80808080u;
+      *reinterpret_cast<lds_w128*>((uintptr_t)(lbase + off)) = w;
+      sfor<1, 4>([&](auto SG) {
+        constexpr int sg = decltype(SG)::value;
+        const u32x4 o = {__builtin_amdgcn_alignbyte(w[1], w[0], sg), __builtin_amdgcn_alignbyte(w[2], w[1], sg),
+                         __builtin_amdgcn_alignbyte(w[3], w[2], sg), __builtin_amdgcn_alignbyte(nx, w[3], sg)};
+        *reinterpret_cast<lds_w128*>((uintptr_t)(lbase + sg * COPY + off)) = o;
+      });
     }
   };
 
@@ -1901,7 +1902,8 @@ static bool plan_mfma_ssd8(const SearchArgs& p, MfmaGeom* g) {
   g->ngxw = g->ngx;  // one workgroup walks all of a tile's groups
   g->km = ME_SSD8_KM;  // L = 16 km candidate rows per chunk
   const int L = 16 * g->km;
-  g->lds = 4 * (L + 8) * ME_SSD8_WP + 16 * 8 + 16 * 4 + (L + 1) * 256;  // 30.7 KB: 5 workgroups per CU
+  // 4 copies + keys + S2 table + the words after each copy granule: 31.8 KB, 5 workgroups per CU
+  g->lds = 4 * (L + 8) * ME_SSD8_WP + 16 * 8 + 16 * 4 + (L + 1) * 256 + (L + 8) * (ME_SSD8_WP / 16) * 4;
   g->ya0 = max(r0 * 8 - S, 0);
   const int ya1 = min(r1 * 8 + S, H);
   g->rp_rows = ya1 - g->ya0;
