@@ -194,6 +194,35 @@ def test_mfma8_vs_valu_and_extremes(engine):
         _check8(engine, ref, cur, 20, f"B8 {tag}")
 
 
+@pytest.mark.parametrize("span", [12, 40])
+def test_mfma8_stripes_from_partial_reference(engine, span):
+    """8x8 SSD stripes whose reference tensor holds only the rows the stripe's
+    windows reach (ref_row0 > 0): the search kernel stages the window straight
+    from that reference (round 5: no r ^ 0x80 plane), so its row offsets and
+    the buffer range at the slice's ends are exercised against the oracle."""
+    import torch
+    w, h, blk = 328, 236, 8
+    rng = np.random.default_rng(77 + span)
+    ref, cur = _pair(rng, h, w, dx=5, dy=-4)
+    omv, oco, _ = O.full_search(ref, cur, blk, span, "ssd", threads=NT)
+    nby, nbx = (h + blk - 1) // blk, w // blk
+    omv, oco = omv.reshape(nby, -1, 2), oco.reshape(nby, -1)
+    for r0, r1 in [(0, 7), (7, 13), (13, nby - 1), (nby - 1, nby), (3, nby)]:
+        y0, y1 = max(r0 * blk - span, 0), min(r1 * blk + span, h)
+        ref_t = torch.from_numpy(ref[y0:y1].copy()).cuda()
+        cur_t = torch.from_numpy(cur[r0 * blk:min(r1 * blk, h)].copy()).cuda()
+        n = (r1 - r0) * omv.shape[1]
+        mv = torch.full((n, 2), -9, dtype=torch.int16, device="cuda")
+        co = torch.zeros(n, dtype=torch.int32, device="cuda")
+        engine.search_stripe_device(ref_t, y0, cur_t, r0 * blk, w, h, blk, span, "ssd", r0, r1, mv, co)
+        torch.cuda.synchronize()
+        msg = f"S{span} rows {r0}:{r1}"
+        np.testing.assert_array_equal(mv.cpu().numpy().reshape(r1 - r0, -1, 2), omv[r0:r1], err_msg=msg)
+        np.testing.assert_array_equal(co.cpu().numpy().view(np.uint32).reshape(r1 - r0, -1), oco[r0:r1],
+                                      err_msg=msg)
+    engine.device_check()
+
+
 def test_mfma8_8k_s128_sampled(engine):
     """BASELINE configs[4] shape with the reference's cost: 7680x4320, 8x8,
     +-128 SSD on the matrix cores, oracle on sampled block rows."""
