@@ -70,6 +70,7 @@ static Tuning read_tuning() {
   env_int("ME_FLOW_SLOTS", 2, 16, &t.flow_slots);
   env_int("ME_PRIO", 0, 1, &t.prio);
   env_int("ME_STRIP", 0, 64, &t.strip);
+  env_int("ME_FAST_RES", 1, 32, &t.fast_res);
   env_int("ME_AHEAD", 1, 2, &t.ahead);
   env_int("ME_ITEM_BATCH", 0, 1, &t.item_batch);
   env_int("ME_FAIR", 0, 3, &t.fair);

@@ -1706,7 +1706,8 @@ static hipError_t launch_fast(const SearchArgs& p, QsadGeom g, int K, const Flow
     const void* fn = (const void*)me_fast_kernel<CC, BB, KK, PP>;                         \
     const hipError_t e_ = lds_attr(fn, g.lds);                                             \
     if (e_ != hipSuccess) return e_;                                                       \
-    const int res = resident_wgs(fn, g.threads, g.lds);                                    \
+    int res = resident_wgs(fn, g.threads, g.lds);                                          \
+    if (tuning().fast_res > 0 && tuning().fast_res < res) res = tuning().fast_res;         \
     const int nwg = ntiles < res * cu_count() ? ntiles : res * cu_count();                 \
     hipLaunchKernelGGL((me_fast_kernel<CC, BB, KK, PP>), dim3((unsigned)nwg), block, g.lds, stream, p, g, jb); \
     return hipGetLastError();                                                              \

@@ -40,6 +40,7 @@ struct Tuning {
   int strip = -1;         // ME_STRIP=0..64: item-kernel tile strips (0 = row-major; -1 = automatic)
   int bw = -1;            // ME_BW=0|1: 16x16 SSD band-walk kernel off / on where it applies (-1 = automatic: on)
   int bw_hb = -1;         // ME_BW_HB=0: a partial bottom row on the lean kernel, not in the band walk
+  int fast_res = 0;       // ME_FAST_RES=1..32: item-kernel workgroups per CU at most (0 = what fits)
   int bw_xt = -1;         // ME_BW_XT=0: uniform segments, no per-XCD tail split
   int bw_seg = 0;         // ME_BW_SEG=1..4096: band-walk block rows per workgroup (0 = automatic)
   int bw_abl = 0;         // ME_BW_ABL=0..1023: band-walk ablations, timing only (results invalid):
