@@ -111,6 +111,7 @@ const char* me_version(void);
  * The environment variable ME_PATH=auto|valu|tiles|lean|prepass sets the
  * initial value (anything else is ignored with a message on stderr). */
 typedef enum {
+  ME_PATH_PROCESS = -1,  /* me_ctx_set_kernel_path only: follow the process-wide path */
   ME_PATH_AUTO = 0,
   ME_PATH_VALU = 1,
   ME_PATH_MFMA_TILES = 2,
@@ -119,8 +120,18 @@ typedef enum {
 } me_path;
 void me_set_kernel_path(me_path path);
 
+/* Per-context kernel path (one host thread per context, as every entry point):
+ * the searches of ctx -- planning, scratch and launch, on every device of the
+ * context and on the pair pipeline's worker threads -- use `path` (an
+ * me_path value) instead of the process-wide one; ME_PATH_PROCESS (the
+ * default of a new context) follows me_set_kernel_path / ME_PATH again.
+ * ME_EINVAL for an unknown value.  Graphs captured earlier keep the kernels
+ * they recorded. */
+me_status me_ctx_set_kernel_path(me_ctx* ctx, int path);
+
 /* The kernel family that ran the most recent search launched in this process
- * (any context, any thread; diagnostics and tests, e.g. that the AUTO path of
+ * (any context, any thread -- me_ctx_last_search_path is the per-context one;
+ * diagnostics and tests, e.g. that the AUTO path of
  * a 16x16 SSD search is the band-walk kernel).  The matrix-core SSD kernels
  * report the kernel of the frame's full-height block rows. */
 typedef enum {
@@ -134,6 +145,11 @@ typedef enum {
   ME_SEARCH_PATH_SSIM = 7            /* SSIM kernels */
 } me_search_path;
 int me_last_search_path(void);
+/* The kernel family (me_search_path) of the most recent search launched by
+ * ctx on its device devs[device_index] (the index into me_create's device
+ * list); ME_SEARCH_PATH_NONE before its first search, -1 for a bad argument.
+ * Per context: a search on another context or thread does not change it. */
+int me_ctx_last_search_path(const me_ctx* ctx, int device_index);
 
 /* Tiling helpers (src/common/prediction_frame.c:9-11). */
 int me_num_blocks(int width, int height, int block_size);

@@ -21,6 +21,7 @@ ME_COMM_TIMEOUT_MS = 60000
 ME_YUV_LUMA, ME_YUV_I420 = 0, 1
 ME_COST_SSD, ME_COST_SAD, ME_COST_SSIM = 0, 1, 2
 ME_PATH_AUTO, ME_PATH_VALU, ME_PATH_MFMA_TILES, ME_PATH_MFMA_LEAN, ME_PATH_MFMA_PREPASS = 0, 1, 2, 3, 4
+ME_PATH_PROCESS = -1
 ME_MAX_BLOCK, ME_MAX_RANGE = 64, 1024
 
 # Every symbol include/me.h declares, with (restype, argtypes).
@@ -35,6 +36,8 @@ _SIGS = {
     "me_num_blocks": (ctypes.c_int, [ctypes.c_int] * 3),
     "me_set_kernel_path": (None, [ctypes.c_int]),
     "me_last_search_path": (ctypes.c_int, []),
+    "me_ctx_set_kernel_path": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "me_ctx_last_search_path": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "me_candidate_count": (ctypes.c_uint64, [ctypes.c_int] * 4),
     "me_full_search": (ctypes.c_int, [ctypes.c_void_p, _u8p, _u8p] + [ctypes.c_int] * 6 +
                        [ctypes.c_void_p, ctypes.c_void_p]),
@@ -114,6 +117,8 @@ def lib():
                                "`python -c 'import __graft_entry__; __graft_entry__.build()'`")
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in _SIGS.items():
+            if os.environ.get("ME_HIP_LIB") and not hasattr(L, name):
+                continue  # an older diagnostic build (A/B runs) may lack newer entry points
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

@@ -120,8 +120,34 @@ static std::atomic<int>& path_code() {
   static std::atomic<int> v{initial_path()};
   return v;
 }
-int kernel_path() { return path_code().load(std::memory_order_relaxed); }
+static thread_local int tl_path = -1;
+static thread_local std::atomic<int>* tl_last = nullptr;
+int kernel_path() { return tl_path >= 0 ? tl_path : path_code().load(std::memory_order_relaxed); }
 void set_kernel_path_code(int v) { path_code().store(v, std::memory_order_relaxed); }
+int path_code_of(int v) {
+  switch (v) {
+    case ME_PATH_AUTO: return 0;
+    case ME_PATH_VALU: return 1;
+    case ME_PATH_MFMA_TILES: return 2;
+    case ME_PATH_MFMA_LEAN: return 3;
+    case ME_PATH_MFMA_PREPASS: return 4;
+    default: return -1;
+  }
+}
+PathScope::PathScope(int path, std::atomic<int>* last) : prev_path(tl_path), prev_last(tl_last) {
+  tl_path = path;
+  tl_last = last;
+}
+PathScope::~PathScope() {
+  tl_path = prev_path;
+  tl_last = prev_last;
+}
+static std::atomic<int> g_last_path{0};
+void note_path(int path) {
+  g_last_path.store(path, std::memory_order_relaxed);
+  if (tl_last) tl_last->store(path, std::memory_order_relaxed);
+}
+int last_path() { return g_last_path.load(std::memory_order_relaxed); }
 
 me_status fail(me_ctx* c, me_status s, const char* fmt, ...) {
   if (c) {
@@ -199,6 +225,7 @@ SearchArgs make_args(const uint8_t* ref, int ref_row0, const uint8_t* cur, int c
 }
 
 me_status attach_scratch(me_ctx* c, Dev& d, SearchArgs& p, bool cap, int batch) {
+  ME_CTX_PATH_SCOPE(c, d);  // the scratch follows the kernels the context's path plans
   p.sched = d.sched;
   {
     const size_t tiles = merge_tiles_needed(p);
@@ -258,6 +285,7 @@ me_status order_on(me_ctx* c, Dev& d, hipStream_t s) {
 }
 
 me_status launch_ordered(me_ctx* c, Dev& d, SearchArgs& p, hipStream_t s) {
+  ME_CTX_PATH_SCOPE(c, d);
   // Captured launches run only when their graph does (me_graph_launch orders
   // it): no ordering and no state change at capture time.
   const bool cap = capturing(s);
@@ -279,6 +307,7 @@ me_status launch_ordered(me_ctx* c, Dev& d, SearchArgs& p, hipStream_t s) {
 
 me_status launch_jobs_ordered(me_ctx* c, Dev& d, const SearchArgs& base, const SearchJob* jobs,
                               int n, hipStream_t s, bool cap) {
+  ME_CTX_PATH_SCOPE(c, d);
   if (!cap) {
     me_status st = order_on(c, d, s);
     if (st != ME_OK) return st;
@@ -615,8 +644,25 @@ const char* me_version(void) { return "me_hip 1 gfx950"; }
 int me_last_search_path(void) { return me::last_path(); }
 
 void me_set_kernel_path(me_path path) {
-  me::set_kernel_path_code(path == ME_PATH_VALU ? 1 : path == ME_PATH_MFMA_TILES ? 2
-                           : path == ME_PATH_MFMA_LEAN ? 3 : path == ME_PATH_MFMA_PREPASS ? 4 : 0);
+  const int code = me::path_code_of((int)path);
+  me::set_kernel_path_code(code < 0 ? 0 : code);
+}
+
+me_status me_ctx_set_kernel_path(me_ctx* c, int path) {
+  if (!c) return ME_EINVAL;
+  if (path == ME_PATH_PROCESS) {
+    c->path = -1;
+    return ME_OK;
+  }
+  const int code = me::path_code_of(path);
+  if (code < 0) return me::fail(c, ME_EINVAL, "me_ctx_set_kernel_path: unknown path %d", path);
+  c->path = code;
+  return ME_OK;
+}
+
+int me_ctx_last_search_path(const me_ctx* c, int device_index) {
+  if (!c || device_index < 0 || (size_t)device_index >= c->last_path.size()) return -1;
+  return c->last_path[(size_t)device_index].load(std::memory_order_relaxed);
 }
 
 me_status me_create(me_ctx** out, const int* device_ids, int n) {
@@ -663,6 +709,8 @@ me_status me_create(me_ctx** out, const int* device_ids, int n) {
     c->devs.push_back(d);
   }
   (void)hipSetDevice(prev);
+  c->last_path = std::vector<std::atomic<int>>(c->devs.size());
+  for (auto& a : c->last_path) a.store(ME_SEARCH_PATH_NONE, std::memory_order_relaxed);
   *out = c;
   return ME_OK;
 }

@@ -2,45 +2,49 @@
 // src/cpu/main.c:18-36, argmin with raster-first ties main.c:53-60, window
 // clamp main.c:73-76) on the matrix cores, walking bands.
 //
-// The decomposition is me_mfma.hip's (SSD = Cc_m + S2(x, y) + 2 X_m(x, y), X_m
-// an i8 GEMM on v_mfma_i32_16x16x64_i8 with the block-major operand layout of
-// me_mfma_bm16_kernel: one block per 16x16 output tile of 16 x positions by 16
-// y positions).  What differs is where S2 = sum over the 16x16 window of
-// (r - 127)^2 comes from.  The block-major kernel reads it from a prepass plane
-// (7.5x the algorithmic HBM bytes at 1080p); me_mfma_bmv_kernel forms it per
-// workgroup and band, once for every block row whose range covers the band
-// (~5x at S = 32).  Here a workgroup owns a strip of C block columns and walks
-// DOWN a segment of block rows band by band: a band is the 16 candidate rows
-// [16 b, 16 b + 16), its S2 is formed once, and every block row in flight (the
-// rows whose search range meets the band: 2 ceil(S/16) + 1 of them) runs its
-// MFMA tiles on it with the same B fragments.  A block row enters at its first
-// band and leaves after its last, so the A fragments of the rows in flight
-// stay in registers (a ring of NS slots per searcher wave).
+// The decomposition is me_mfma.hip's: SSD(block m, x, y) = Cc_m + S2(x, y) +
+// 2 X_m(x, y) with c'' = 127 - c and r' = r - 128 (both exact i8: c ^ 0x7F,
+// r ^ 0x80), X_m = sum c'' r' an i8 GEMM on v_mfma_i32_16x16x64_i8 with the
+// block-major operand layout of me_mfma_bm16_kernel (one block per 16x16
+// output tile of 16 x positions by 16 y positions), Cc_m = sum (c''^2 + 2 c'')
+// per block and S2 = sum (r - 127)^2 over the 16x16 window per position.
+// What differs from the block-major kernel is where S2 comes from: that
+// kernel reads a prepass plane (7.5x the algorithmic HBM bytes at 1080p).
+// Here a workgroup owns a strip of C block columns and walks DOWN a segment of
+// block rows band by band: a band is the 16 candidate rows [16 b, 16 b + 16), its S2 is
+// formed once in LDS, and every block row in flight (the rows whose search
+// range meets the band: 2 ceil(S/16) + 1 of them) runs its MFMA tiles on it
+// with the same B fragments.  A block row enters at its first band and leaves
+// after its last, so the A fragments of the rows in flight stay in registers
+// (a ring of NS slots per searcher wave).
 //
-//   waves      16 (1,024 threads, one workgroup per CU, <= 128 VGPRs), two
-//              roles: three searchers and one producer per SIMD.
+//   waves      16 (1,024 threads, one workgroup per CU, <= 128 VGPRs): 12
+//              searchers and 4 producers, three searchers and one producer
+//              per SIMD.
 //   searchers  waves 0..11: block column w % C of the strip, row class w / C
 //              (12 / C classes split a column's rows in flight, two ring slots
 //              each: A fragments of 2 rows = 64 VGPRs).  Per band and tile: 8 B
-//              fragments (ds_read_b128, two fragments ahead) and one P0
-//              vector; 8 MFMAs per row in flight, the rows interleaved
-//              (independent accumulation chains), no MFMA for a free slot;
-//              keys as the block-major kernel's.  Nothing else but the rows'
-//              entries and exits.
-//   producers  waves 12..15: the window slabs (LDS DMA) and S2: band m is
-//              produced by producer (m - first band) % 4 during the 4
-//              iterations before it is searched (46 steps of a sliding 16-row
-//              sum, 12 per iteration), lane = 4 positions (one v_dot4 per
-//              window row of 4 bytes), the 16-wide horizontal sum by DPP
-//              within 16-lane rows, the result stored as the key's position
-//              term P0 = (S2 << 6) + 2^29 + 64 + (x & 3); the first 16 steps
-//              also store slab m XOR-ed with 0x80.  Their VALU work runs beside
-//              the searchers' MFMAs on the same SIMDs.
-//   LDS        the window in 16-row slabs: a raw ring (6 slabs ahead) read by
-//              the producers, and the slabs XOR-ed with 0x80 (the MFMA B
-//              operand r - 128) in a ring of 5 + a mirror of slot 0, so a
-//              band's 31 rows are contiguous; 5 P0 planes (the band searched +
-//              the 4 in production)
+//              fragments (ds_read_b128, three ahead through a ring of 4) and
+//              one P0 vector; 8 MFMAs per row in flight, no MFMA for a free
+//              slot; keys (X << 7) + P0 and a v_min3 per two keys.
+//   producers  waves 12..15: producer p forms bands first + p, + 4, ...: it
+//              DMAs the band's 31 window rows into the band's ring slot,
+//              XORs them with 0x80 in place (b128 LDS ops: the MFMA B operand
+//              r'), then 46 steps of a sliding 16-row sum (16 rows in, then
+//              15 x (row out, row in)), lane = 4 positions (one v_dot4 of
+//              u = 127 - r = ~r' with itself per 4 bytes), the 16-wide
+//              horizontal sum by DPP within 16-lane rows, stored as the key's
+//              position term P0 = (S2 << 6) + 2^29 + 64 + idx.  Their VALU work runs
+//              beside the searchers' MFMAs on the same SIMDs.
+//   hand-off   a ring of BW_K = 8 band slots (window + P0 plane each), no
+//              barrier after the start: the producer publishes ready[k] =
+//              band, the searchers bump done[k] when they are through with
+//              it, and the producer of band b + 8 waits for every searcher
+//              before reusing the slot (bounded waits: ME_EDEVICE, never a
+//              hang).
+//   partial    a partial bottom block row (height < 16) is searched by the
+//   bottom row producers of the last segment after their bands, on hb-row
+//              S2 planes they form beside the bands.
 //
 // HBM: the reference rows of the strip window, once per workgroup (adjacent
 // strips share them through the XCD's L2: consecutive workgroups are adjacent
@@ -75,9 +79,10 @@ constexpr int BW_PW = 4;             // producer waves per workgroup (one per SI
 
 #ifdef ME_STAMPS
 // Diagnostic build only (libme_hip_stamps.so): per workgroup and wave, the
-// s_memtime cycles spent in each phase, summed over the bands: [start,
-// entries / producer's slot wait, fetch, tiles, band end, production, ready
-// wait, bands] (tools/bw_stamps.py).
+// s_memtime cycles spent in each phase, summed over the bands: searchers
+// [start, entries, fetch, tiles, band end, -, ready wait, bands], producers
+// [start, slot wait + DMA issue, DMA wait, partial-row S2, publish,
+// production, partial-row search, bands] (tools/bw_stamps.py).
 constexpr int BW_STW = 16;  // waves per workgroup slot
 __device__ unsigned long long g_bwstamps[BW_STW * 8 * 4096];
 #define BW_T0() unsigned long long bw_t = __builtin_amdgcn_s_memtime()
@@ -95,8 +100,11 @@ constexpr int BW_WIN_ROWS = 31;      // window rows of a band: 16 b .. 16 b + 30
 // done[k] = searcher waves finished with it (the producer of band b + K
 // waits for all of them, then reuses the slot).
 struct BwCtl {
+  uint32_t trash[4];  // (16-byte aligned) the P0 store of producer lanes without an output
   int ready[BW_K];
   int done[BW_K];
+  int hbready[BW_K];  // the partial row's plane of band lo_h + i formed
+  int hbcnt[BW_K];    // the partial row's bands searched, per block column
 };
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -120,10 +128,11 @@ __host__ __device__ inline int bw_lds_bytes(int lp, int pp, int ns, int nsw) {
   return BW_K * bw_win(lp) + BW_K * 16 * pp * 4 + nsw * 16 * BW_CREC + nsw * 256 + nsw * ns * 8 +
          (int)sizeof(BwCtl);
 }
-// the partial bottom row's extra LDS: its nhb S2 planes, the producers' row
-// records and keys
+// the partial bottom row's extra LDS: its nhb S2 planes and a key per block
+// column of the strip
 __host__ __device__ inline int bw_lds_hb_bytes(int pp, int ns, int nhb) {
-  return nhb ? nhb * 16 * pp * 4 + BW_PW * (16 * BW_CREC + ns * 8) : 0;
+  (void)ns;
+  return nhb ? nhb * 16 * pp * 4 + BW_K * 8 : 0;  // its planes, a key per block column
 }
 
 // Bounded spin on an LDS word (the handshake's ordering argument says it
@@ -158,7 +167,11 @@ __device__ __forceinline__ bool bw_wait(const SearchArgs& p, int lane, Pred ok) 
 // band times; its st segments ~ rows / st + that).  Launch order within an
 // XCD is blockIdx order, so the segments run last.
 struct BwItem {
-  int u, seg, rows;
+  // segment seg of item u: block rows [seg rows + (seg ? top : 0), + rows (+ top
+  // for seg 0)), clipped to the job's; the last one of an uneven plan takes
+  // the rest (last)
+  int u, seg, rows, top;
+  bool last;
 };
 __host__ __device__ inline void bw_xcd_split(int nx, int cx, int rows, int* main, int* kx, int* st,
                                              int* L) {
@@ -176,17 +189,17 @@ __device__ __forceinline__ BwItem bw_item(const MfmaGeom& g, int jobs) {
     const int per = g.bw_strips * g.bw_segs, j = lin / per;
     lin -= j * per;
     const int seg = lin / g.bw_strips;
-    return {j * g.bw_strips + lin - seg * g.bw_strips, seg, g.bw_seg_rows};
+    return {j * g.bw_strips + lin - seg * g.bw_strips, seg, g.bw_seg_rows, g.bw_seg_top, seg == g.bw_segs - 1};
   }
   const int b = (int)blockIdx.x, x = b & 7, m = b >> 3;
   const int U = jobs * g.bw_strips, q = U >> 3, rem = U & 7;
   const int nx = q + (x < rem ? 1 : 0), u0 = x * q + min(x, rem);
   int mainx, kx, st, L;
   bw_xcd_split(nx, g.bw_cx, g.bw_seg_rows, &mainx, &kx, &st, &L);
-  if (m < mainx) return {u0 + m, 0, g.bw_seg_rows};
+  if (m < mainx) return {u0 + m, 0, g.bw_seg_rows, 0, true};
   const int t = m - mainx;
-  if (t >= kx * st) return {-1, 0, 0};
-  return {u0 + mainx + t % kx, t / kx, L};
+  if (t >= kx * st) return {-1, 0, 0, 0, false};
+  return {u0 + mainx + t % kx, t / kx, L, 0, false};
 }
 
 template <int C, int NS, int LP, int NSW, int PW, bool ABL>
@@ -199,11 +212,11 @@ __global__ __launch_bounds__(64 * (NSW + PW), 4) void me_mfma_bw_kernel(SearchAr
   uint8_t* xw = smem;
   int* p0 = reinterpret_cast<int*>(xw + BW_K * WIN);
   // (the partial bottom row's S2 planes, g.bw_hb of them, follow the ring)
-  const int nwr = NSW + (g.bw_hb ? PW : 0);  // waves with row records and keys
+  const int nkeys = NSW * NS + (g.bw_hb ? BW_K : 0);  // the searchers' slots, the partial row's columns
   uint8_t* crec_all = reinterpret_cast<uint8_t*>(p0 + (BW_K + g.bw_hb) * P0PLANE);
-  uint8_t* stage_all = crec_all + nwr * 16 * BW_CREC;
+  uint8_t* stage_all = crec_all + NSW * 16 * BW_CREC;
   unsigned long long* keys = reinterpret_cast<unsigned long long*>(stage_all + NSW * 256);
-  BwCtl* ctl = reinterpret_cast<BwCtl*>(keys + nwr * NS);
+  BwCtl* ctl = reinterpret_cast<BwCtl*>(keys + nkeys);
 
   const int tid = (int)threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -219,8 +232,8 @@ __global__ __launch_bounds__(64 * (NSW + PW), 4) void me_mfma_bw_kernel(SearchAr
     const int j = it.u / g.bw_strips;
     strip = it.u - j * g.bw_strips;
     mfma_job(jb, j, p, g);
-    r0 = g.row0 + it.seg * it.rows;
-    r1 = min(r0 + it.rows, g.row0 + g.nrows);
+    r0 = g.row0 + it.seg * it.rows + (it.seg ? it.top : 0);
+    r1 = it.last ? g.row0 + g.nrows : min(g.row0 + (it.seg + 1) * it.rows + it.top, g.row0 + g.nrows);
   }
   const int bc0 = strip * C, ncol = min(C, g.nbx - bc0);
   const int tc0 = max(16 * bc0 - S, 0) >> 4;  // first tile column of the strip window
@@ -250,16 +263,15 @@ __global__ __launch_bounds__(64 * (NSW + PW), 4) void me_mfma_bw_kernel(SearchAr
   const __amdgpu_buffer_rsrc_t rref =
       __builtin_amdgcn_make_buffer_rsrc((void*)p.ref, (short)0, p.ref_bytes, 0x00020000);
   // V(row) = sum of 16 window rows of H, H(row, x) = sum over the 4 bytes at
-  // x of (r - 127)^2 (u = r ^ 0x7F = 127 - r as an i8: one v_dot4 per 4
-  // bytes).  Lane (row R, l) owns the 4 positions of group pg = 13 R + l: the
+  // x of (r - 127)^2 (u = 127 - r = ~(r ^ 0x80) as an i8, from the XOR-ed
+  // window byte: one v_dot4 per 4 bytes).  Lane (row R, l) owns the 4 positions of group pg = 13 R + l: the
   // 16-lane rows overlap by 3 groups, so a group's three right neighbours are
   // in its own row (l < 13 outputs).
   const int pg = 13 * (lane >> 4) + (lane & 15);
   const bool pout = (lane & 15) < 13 && 4 * pg < npos;
-  const bool pxor = (lane & 15) < 13 && 4 * pg < LP;  // writes the XOR-ed window bytes 4 pg .. 4 pg + 3
   v4i V = {0, 0, 0, 0}, R = {0, 0, 0, 0};  // sums of the rows added / removed
-  auto h_acc = [&](uint32_t w0, uint32_t w1, v4i acc) {  // acc + H of the bytes (w0, w1)
-    const uint32_t u0 = w0 ^ 0x7F7F7F7Fu, u1 = w1 ^ 0x7F7F7F7Fu;
+  auto h_acc = [&](uint32_t w0, uint32_t w1, v4i acc) {  // acc + H of the XOR-ed window bytes (w0, w1)
+    const uint32_t u0 = ~w0, u1 = ~w1;  // u = 127 - r = ~(r - 128)
     const uint32_t u[4] = {u0, __builtin_amdgcn_alignbyte(u1, u0, 1),
                            __builtin_amdgcn_alignbyte(u1, u0, 2),
                            __builtin_amdgcn_alignbyte(u1, u0, 3)};
@@ -274,24 +286,26 @@ __global__ __launch_bounds__(64 * (NSW + PW), 4) void me_mfma_bw_kernel(SearchAr
   // strip-relative tile, so the search adds nothing per tile (a lane's keys
   // share its x & 12, and idx orders its candidates by x)
   const uint32_t p0k = (1u << 29) + 64u + 4u * (uint32_t)(pg >> 2);
+  // Every lane stores (no exec-mask branch per row, and the DPP adds fuse):
+  // a lane without an output (the 3 overlap lanes of each 16-lane row, groups
+  // past the window) stores into ctl->trash.
   auto out_row = [&](int k, int j) {
     v4i T, Q, D;
 #pragma unroll
     for (int r = 0; r < 4; r++) D[r] = V[r] - R[r];
 #pragma unroll
-    for (int r = 0; r < 4; r++) T[r] = D[r] + __builtin_amdgcn_update_dpp(0, D[r], 0x101, 0xF, 0xF, false);
+    for (int r = 0; r < 4; r++) T[r] = D[r] + __builtin_amdgcn_update_dpp(0, D[r], 0x101, 0xF, 0xF, true);
 #pragma unroll
-    for (int r = 0; r < 4; r++) Q[r] = T[r] + __builtin_amdgcn_update_dpp(0, T[r], 0x102, 0xF, 0xF, false);
-    if (pout) {
-      v4i o;
+    for (int r = 0; r < 4; r++) Q[r] = T[r] + __builtin_amdgcn_update_dpp(0, T[r], 0x102, 0xF, 0xF, true);
+    v4i o;
 #pragma unroll
-      for (int r = 0; r < 4; r++) o[r] = (int)(((uint32_t)Q[r] << 6) + p0k + (uint32_t)r);
-      // the lane's base recomputed per row (opaque): hoisted, the 16 row
-      // addresses pinned 16 VGPRs and spilled
-      typedef __attribute__((address_space(3))) v4i lds_v4i;
-      const uint32_t pa = (uint32_t)opaque((int)lds_addr(p0 + 4 * pg)) + 4u * (uint32_t)(k * P0PLANE + j * PP);
-      *reinterpret_cast<lds_v4i*>((uintptr_t)pa) = o;
-    }
+    for (int r = 0; r < 4; r++) o[r] = (int)(((uint32_t)Q[r] << 6) + p0k + (uint32_t)r);
+    // the lane's base recomputed per row (opaque): hoisted, the 16 row
+    // addresses pinned 16 VGPRs and spilled
+    typedef __attribute__((address_space(3))) v4i lds_v4i;
+    const uint32_t pa = pout ? (uint32_t)opaque((int)lds_addr(p0 + 4 * pg)) + 4u * (uint32_t)(k * P0PLANE + j * PP)
+                             : lds_addr(ctl->trash);
+    *reinterpret_cast<lds_v4i*>((uintptr_t)pa) = o;
   };
   // The band's window rows (16 m .. 16 m + 30, LP bytes from column 16 tc0)
   // by LDS DMA straight into its slot, then XOR-ed there in place by the
@@ -312,35 +326,37 @@ __global__ __launch_bounds__(64 * (NSW + PW), 4) void me_mfma_bw_kernel(SearchAr
     }
   };
   // Band m's 46 steps: 0..15 add window rows 0..15 (row 0 out after 15), then
-  // for j = 1..15: remove row j - 1, add row j + 15, row j out.  Every "add"
-  // step reads its row raw and writes it back XOR-ed with 0x80 (r - 128 as an
-  // i8: the MFMA B operand; the lanes read the row before any writes it, and
-  // lanes l < 13 hold each 4 bytes once); a "remove" step reads its row
-  // XOR-ed (u = r ^ 0x7F = w ^ 0xFF).  Steps [O0, O1) (compile-time, at most
-  // 12): the rows of all the steps are read first (one LDS latency).
+  // for j = 1..15: remove row j - 1, add row j + 15, row j out.  Every step
+  // reads its row XOR-ed (xor_win ran first: u = 127 - r = ~w).  Steps
+  // [O0, O1) (compile-time, at most 12): the rows of all the steps are read
+  // first (one LDS latency).
   auto step_row = [](int o) { return o < 16 ? o : ((o - 16) & 1) ? ((o - 16) >> 1) + 16 : ((o - 16) >> 1); };
-  auto steps = [&](auto c0, auto c1, int k) __attribute__((always_inline)) {
+  // Batches of steps are software-pipelined: the rows of batch i + 1 are
+  // read (ds_read2_b32) before batch i is computed, so an LDS round trip
+  // under the searchers' b128 traffic overlaps a batch of VALU work.
+  auto load = [&](auto c0, auto c1, int k, uint32_t (&w0)[12], uint32_t (&w1)[12]) __attribute__((always_inline)) {
     constexpr int O0 = decltype(c0)::value, O1 = decltype(c1)::value;
-    typedef __attribute__((address_space(3))) uint32_t lds_u32;
     const uint32_t xa = (uint32_t)opaque((int)lds_addr(xw + k * WIN)) + 4u * (uint32_t)pg;
-    uint32_t w0[12], w1[12];
 #pragma unroll
     for (int o = O0; o < O1; o++) {
       w0[o - O0] = ld32(xa + (uint32_t)(step_row(o) * LP));
       w1[o - O0] = ld32(xa + (uint32_t)(step_row(o) * LP + 4));
     }
+  };
+  auto steps = [&](auto c0, auto c1, int k, const uint32_t (&w0)[12], const uint32_t (&w1)[12]) __attribute__((always_inline)) {
+    constexpr int O0 = decltype(c0)::value, O1 = decltype(c1)::value;
 #pragma unroll
     for (int o = O0; o < O1; o++) {
       const bool add = o < 16 || ((o - 16) & 1);
+      // the window is XOR-ed already (xor_win): w = r ^ 0x80 (h_acc takes ~w)
       const uint32_t x0 = w0[o - O0], x1 = w1[o - O0];
-      if (add && pxor) *reinterpret_cast<lds_u32*>((uintptr_t)(xa + (uint32_t)(step_row(o) * LP))) = x0 ^ 0x80808080u;
       if (o < 16) {
         const v4i z = {0, 0, 0, 0};
         V = h_acc(x0, x1, o == 0 ? z : V);
         if (o == 0) R = z;
         if (o == 15) out_row(k, 0);
       } else if (!add) {
-        R = h_acc(x0 ^ 0x80808080u, x1 ^ 0x80808080u, R);
+        R = h_acc(x0, x1, R);
       } else {
         V = h_acc(x0, x1, V);
         out_row(k, ((o - 16) >> 1) + 1);
@@ -354,27 +370,78 @@ __global__ __launch_bounds__(64 * (NSW + PW), 4) void me_mfma_bw_kernel(SearchAr
   auto produce_hb = [&](int m) {
     const int k = BW_K + (m - lo_h);
     const uint32_t xa = (uint32_t)opaque((int)lds_addr(xw + (m % BW_K) * WIN)) + 4u * (uint32_t)pg;
-    auto rd = [&](int t, v4i acc) {
-      return h_acc(ld32(xa + (uint32_t)(t * LP)) ^ 0x80808080u, ld32(xa + (uint32_t)(t * LP + 4)) ^ 0x80808080u, acc);
-    };
     const v4i z = {0, 0, 0, 0};
     V = z;
     R = z;
+    // rows in groups of 4 (one LDS round trip per group, not per row: this
+    // runs before the band is published)
 #pragma unroll 1
-    for (int t = 0; t < hbh; t++) V = rd(t, V);
+    for (int t0 = 0; t0 < hbh; t0 += 4) {  // t0 + 3 <= 15: inside the window
+      uint32_t a0[4], a1[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        a0[i] = ld32(xa + (uint32_t)((t0 + i) * LP));
+        a1[i] = ld32(xa + (uint32_t)((t0 + i) * LP + 4));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; i++)
+        if (t0 + i < hbh) V = h_acc(a0[i], a1[i], V);
+    }
     out_row(k, 0);
 #pragma unroll 1
-    for (int j = 1; j < 16; j++) {
-      R = rd(j - 1, R);
-      V = rd(j + hbh - 1, V);
-      out_row(k, j);
+    for (int j0 = 1; j0 < 16; j0 += 4) {  // rows j - 1 and j + hbh - 1 <= 29
+      uint32_t r0w[4], r1w[4], a0[4], a1[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const int j = min(j0 + i, 15);
+        r0w[i] = ld32(xa + (uint32_t)((j - 1) * LP));
+        r1w[i] = ld32(xa + (uint32_t)((j - 1) * LP + 4));
+        a0[i] = ld32(xa + (uint32_t)((j + hbh - 1) * LP));
+        a1[i] = ld32(xa + (uint32_t)((j + hbh - 1) * LP + 4));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        if (j0 + i > 15) break;
+        R = h_acc(r0w[i], r1w[i], R);
+        V = h_acc(a0[i], a1[i], V);
+        out_row(k, j0 + i);
+      }
     }
   };
+  // The band's window XOR-ed with 0x80 in place (r - 128 as an i8: the MFMA
+  // B operand), 16 bytes per lane, before the production reads it: one pass
+  // of b128 LDS ops instead of a masked 4-byte write per lane and window row
+  // inside the steps (31 exec-mask branches per band).
+  constexpr int XN = (WIN + 1023) / 1024;
+  static_assert(WIN % 16 == 0, "window slots of whole 16-byte granules");
+  auto xor_win = [&](int k) __attribute__((always_inline)) {
+    typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
+    const uint32_t base = (uint32_t)opaque((int)lds_addr(xw + k * WIN)) + 16u * (uint32_t)lane;
+    u32x4 v[XN];
+#pragma unroll
+    for (int i = 0; i < XN; i++)
+      if (i < XN - 1 || 1024 * i + 16 * lane < WIN) v[i] = *reinterpret_cast<lds_u32x4*>((uintptr_t)(base + 1024u * i));
+#pragma unroll
+    for (int i = 0; i < XN; i++)
+      if (i < XN - 1 || 1024 * i + 16 * lane < WIN)
+        *reinterpret_cast<lds_u32x4*>((uintptr_t)(base + 1024u * i)) = v[i] ^ 0x80808080u;
+  };
   auto produce = [&](int k) __attribute__((always_inline)) {
-    steps(std::integral_constant<int, 0>{}, std::integral_constant<int, 12>{}, k);
-    steps(std::integral_constant<int, 12>{}, std::integral_constant<int, 24>{}, k);
-    steps(std::integral_constant<int, 24>{}, std::integral_constant<int, 36>{}, k);
-    steps(std::integral_constant<int, 36>{}, std::integral_constant<int, BW_OPS>{}, k);
+    using I0 = std::integral_constant<int, 0>;
+    using I12 = std::integral_constant<int, 12>;
+    using I24 = std::integral_constant<int, 24>;
+    using I36 = std::integral_constant<int, 36>;
+    using IE = std::integral_constant<int, BW_OPS>;
+    xor_win(k);
+    uint32_t a0[12], a1[12], b0[12], b1[12];
+    load(I0{}, I12{}, k, a0, a1);
+    load(I12{}, I24{}, k, b0, b1);
+    steps(I0{}, I12{}, k, a0, a1);
+    load(I24{}, I36{}, k, a0, a1);
+    steps(I12{}, I24{}, k, b0, b1);
+    load(I36{}, IE{}, k, b0, b1);
+    steps(I24{}, I36{}, k, a0, a1);
+    steps(I36{}, IE{}, k, b0, b1);
   };
 
   // ================================ searchers
@@ -500,11 +567,15 @@ __global__ __launch_bounds__(64 * (NSW + PW), 4) void me_mfma_bw_kernel(SearchAr
     }
   };
 
-  // The partial bottom row, block column c of the strip (a producer wave, once
-  // its bands are formed): its A fragments from its hbh cur rows (rows below
-  // as c'' = 0: they add nothing to X or Cc), one MFMA slot, the keys on its
-  // hbh-row S2 planes, its best over the bands -> its record.
-  auto hb_search = [&](int c) {
+  // The partial bottom row (block row hbrow, hbh < 16 rows) at block column
+  // c of the strip and band b, one of its bands lo_h .. hbrow: a searcher
+  // wave once its own walk is done (the pairs are dealt over all searcher
+  // waves: 12 at 1080p, one each).  Its A fragments from its hbh cur rows
+  // (rows below as c'' = 0: they add nothing to X or Cc), one MFMA slot, the
+  // keys on the band's hbh-row S2 plane; the band's best over the lanes into
+  // the column's 64-bit key, and the column's last band to finish writes its
+  // record.
+  auto hb_pair = [&](int c, int b, int nbh) {
     const int bxc = 16 * (bc0 + c);
     const int xl = max(bxc - S, 0), xh = min(bxc + S, W - 16);
     const int ia = xl >> 4, ib = xh >> 4;
@@ -541,60 +612,56 @@ __global__ __launch_bounds__(64 * (NSW + PW), 4) void me_mfma_bw_kernel(SearchAr
 #pragma unroll
       for (int e = 0; e < 4; e++) Ah[q][e] = (int)__builtin_amdgcn_alignbyte(d[e + 1], d[e], sh);
     }
-    const int ylo = max(16 * hbrow - S, 0), yhi = H - hbh;
-    uint32_t best = ~0u;
-    int bbest = 0;
+    // the band's window (slot b % K: no later band of this segment reuses
+    // it) and hbh-row plane, published by its producer
+    const int kw = b % BW_K;
+    if (!bw_wait(p, lane, [&] {
+          return __hip_atomic_load(&ctl->hbready[b - lo_h], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
+        }))
+      return false;
+    const uint32_t xb = lds_addr(xw + kw * WIN) + (uint32_t)((n + (h >> 1)) * LP + 16 * (h & 1) - 16 * tc0);
+    const uint32_t pb = lds_addr(p0 + (BW_K + b - lo_h) * P0PLANE) + (uint32_t)((n * PP + 4 * h - 16 * tc0) * 4);
+    uint32_t bc = ~0u;
 #pragma unroll 1
-    for (int b = lo_h; b <= hbrow; b++) {
-      const int kw = b % BW_K;
-      if (!bw_wait(p, lane, [&] {
-            return __hip_atomic_load(&ctl->ready[kw], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == b;
-          }))
-        return false;
-      const uint32_t xb = lds_addr(xw + kw * WIN) + (uint32_t)((n + (h >> 1)) * LP + 16 * (h & 1) - 16 * tc0);
-      const uint32_t pb = lds_addr(p0 + (BW_K + b - lo_h) * P0PLANE) + (uint32_t)((n * PP + 4 * h - 16 * tc0) * 4);
-      uint32_t bc = ~0u;
-#pragma unroll 1
-      for (int i = ia; i <= ib; i++) {
-        v4i acc = {0, 0, 0, 0};
+    for (int i = ia; i <= ib; i++) {
+      // the tile's 8 fragments and P0 vector read first: one LDS round trip
+      v4i f[8];
 #pragma unroll
-        for (int q = 0; q < 8; q++) acc = MFMA16(Ah[q], ldv4(xb + (uint32_t)(16 * i + 2 * q * LP)), acc, 0, 0, 0);
-        const v4i pv = ldv4(pb + (uint32_t)(64 * i));
-        uint32_t k[4];
+      for (int q = 0; q < 8; q++) f[q] = ldv4(xb + (uint32_t)(16 * i + 2 * q * LP));
+      const v4i pv = ldv4(pb + (uint32_t)(64 * i));
+      v4i acc = {0, 0, 0, 0};
 #pragma unroll
-        for (int r = 0; r < 4; r++) {
-          const int xx = 16 * i + 4 * h + r;
-          k[r] = ((uint32_t)acc[r] << 7) + ((uint32_t)pv[r] | ((xx < xl || xx > xh) ? 0x80000000u : 0u));
-        }
-        bc = umin3(umin3(bc, k[0], k[1]), k[2], k[3]);
+      for (int q = 0; q < 8; q++) acc = MFMA16(Ah[q], f[q], acc, 0, 0, 0);
+      uint32_t k[4];
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int xx = 16 * i + 4 * h + r;
+        k[r] = ((uint32_t)acc[r] << 7) + ((uint32_t)pv[r] | ((xx < xl || xx > xh) ? 0x80000000u : 0u));
       }
-      const int y = 16 * b + n;
-      if (y >= ylo && y <= yhi && (bc >> 6) < (best >> 6)) {
-        best = bc;
-        bbest = b;
-      }
+      bc = umin3(umin3(bc, k[0], k[1]), k[2], k[3]);
     }
-    // best over the lanes -> the block's record (as emit)
-    unsigned long long* kp = keys + wave * NS;
-    const uint32_t hk = best >> 6;
-    if (hk < (1u << 25)) {
+    const int ylo = max(16 * hbrow - S, 0), yhi = H - hbh;
+    const int y = 16 * b + n;
+    // the band's best over the lanes -> the column's key (cost, dy, dx)
+    unsigned long long* kp = keys + NSW * NS + c;
+    const uint32_t hk = bc >> 6;
+    if (y >= ylo && y <= yhi && hk < (1u << 25)) {
       const uint32_t cost = hk - 1u - (1u << 23) + (uint32_t)ccv;
-      const int idx = (int)(best & 63u);
+      const int idx = (int)(bc & 63u);
       const int dx = 16 * (tc0 + (idx >> 2)) + 4 * h + (idx & 3) - bxc;
-      const int dy = 16 * bbest + n - 16 * hbrow;
+      const int dy = y - 16 * hbrow;
       const unsigned long long key = ((unsigned long long)cost << 32) |
                                      ((uint32_t)(dy + 32768) << 16) | (uint32_t)(dx + 32768);
       asm volatile("ds_min_u64 %0, %1" : : "v"(lds_addr(kp)), "v"(key) : "memory");
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (lane == 0) {
-      const unsigned long long kk = *kp;
+    if (lane == 0 &&
+        __hip_atomic_fetch_add(&ctl->hbcnt[c], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP) == nbh - 1) {
+      const unsigned long long kk = *kp;  // every band of the column folded in
       const int out = (hbrow - p.block_row_begin) * p.nbx + bc0 + c;
       store_mv(p.mv, out, kk);
       if (p.cost) p.cost[out] = (uint32_t)(kk >> 32);
-      *kp = ~0ull;
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     return true;
   };
 
@@ -602,10 +669,12 @@ __global__ __launch_bounds__(64 * (NSW + PW), 4) void me_mfma_bw_kernel(SearchAr
   unsigned long long bw_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
   BW_T0();
-  if (tid < nwr * NS) keys[tid] = ~0ull;
+  if (tid < nkeys) keys[tid] = ~0ull;
   if (tid < BW_K) {
     ctl->ready[tid] = -(1 << 30);
     ctl->done[tid] = 0;
+    ctl->hbready[tid] = 0;
+    ctl->hbcnt[tid] = 0;
   }
   __syncthreads();  // the only barrier: keys and handshake words initialised
   BW_ACC(0);
@@ -627,30 +696,52 @@ __global__ __launch_bounds__(64 * (NSW + PW), 4) void me_mfma_bw_kernel(SearchAr
       dma_win(m, k);
       return true;
     };
+    // (tuning build: bit 16 raises the producers' issue priority for the
+    // whole walk, bit 32 for the first ring of bands only)
+    if (ABL && (g.bw_abl & 48)) __builtin_amdgcn_s_setprio(2);
+    // Band m + PW's window is DMA'd before band m is produced when its slot
+    // is free already (the DMA then lands during the production), otherwise
+    // right after band m is published: a producer never waits for the
+    // searchers before producing a band whose window it has (waiting there
+    // held every producer to the searchers' pace, one band behind: the
+    // slot-wait was ~20 % of a single-frame segment).
+    auto slot_free = [&](int m) {
+      return m - BW_K < bfirst ||
+             __hip_atomic_load(&ctl->done[m % BW_K], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= nact;
+    };
     bool ok = bfirst + pw > blast_p || claim(bfirst + pw);
 #pragma unroll 1
     for (int m = bfirst + pw; ok && m <= blast_p; m += PW) {
       const int k = m % BW_K;
+      if (ABL && (g.bw_abl & 32) && m >= bfirst + BW_K) __builtin_amdgcn_s_setprio(0);
       const bool next = m + PW <= blast_p;
-      if (next) ok = claim(m + PW);
+      const bool ahead = next && __builtin_amdgcn_readfirstlane(slot_free(m + PW) ? 1 : 0);
+      if (ahead) ok = claim(m + PW);  // (free: no wait)
       BW_ACC(1);
       // band m's window landed (band m + PW's DMA may still be in flight)
-      if (next)
+      if (ahead)
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DMA_N) : "memory");
       else
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (!(ABL && (g.bw_abl & 1))) {
-        produce(k);
-        if (hbk && m >= lo_h) produce_hb(m);
-      }
+      BW_ACC(2);  // (stamps, producers: DMA wait)
+      if (!(ABL && (g.bw_abl & 1))) produce(k);
       BW_ACC(5);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the window and P0 stores landed
       if (lane == 0) __hip_atomic_store(&ctl->ready[k], m, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      BW_ACC(4);  // (stamps, producers: publish)
+      // the partial row's plane of this band, after the band is published
+      // (the searchers go on with it meanwhile)
+      if (hbk && m >= lo_h) {
+        if (!(ABL && (g.bw_abl & 1))) produce_hb(m);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0) __hip_atomic_store(&ctl->hbready[m - lo_h], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        BW_ACC(3);  // (stamps, producers: the partial row's S2)
+      }
+      if (next && !ahead) ok = claim(m + PW);
+      BW_ACC(1);
     }
-    // then the partial bottom row: producer pw takes columns pw, pw + PW, ...
-#pragma unroll 1
-    for (int c = pw; ok && hbk && c < ncol; c += PW) ok = hb_search(c);
-  } else if (hascol) {
+  } else {
+   if (hascol) {
     fetch(bfirst);
     if (!(ABL && (g.bw_abl & 4)))
       for (int br = pe0; br < pe1; br += WPC)
@@ -786,6 +877,16 @@ __global__ __launch_bounds__(64 * (NSW + PW), 4) void me_mfma_bw_kernel(SearchAr
           enter(br, br == pe0 ? staged() : cur_row(br));
       BW_ACC(1);
     }
+   }
+    // then the partial bottom row: its (column, band) pairs over every
+    // searcher wave
+    if (hbk) {
+      const int nbh = hbrow - lo_h + 1;
+#pragma unroll 1
+      for (int t = wave; t < ncol * nbh; t += NSW)
+        if (!hb_pair(t % ncol, lo_h + t / ncol, nbh)) break;
+      BW_ACC(5);  // (stamps, searchers: the partial row's search)
+    }
   }
 #ifdef ME_STAMPS
   if (lane == 0 && blockIdx.x < 4096) {
@@ -850,31 +951,62 @@ bool plan_bw(const SearchArgs& p, MfmaGeom* g, int jobs) {
   g->bw_lp = lp;
   g->bw_pp = pp;
   g->bw_strips = (g->nbx + C - 1) / C;
-  // Segment rows: rounds of resident workgroups x (segment bands + the
-  // 2 ceil(S/16) extra bands + ~2 bands of prologue), the smallest
-  int best_t = 1 << 30, best_l = rows;
-  const int cus = bw_cu_count() * wgs_cu, extra = 2 * ((S + 15) / 16) + 2;
+  // Segments: rounds of resident workgroups x (the most bands one segment
+  // walks + ~2 bands of prologue), the smallest.  A segment of rows [r0, r1)
+  // walks bands lo(r0) .. hi(r1 - 1), 2 ceil(S/16) more than its rows in the
+  // middle of the frame but only ceil(S/16) more at the top and bottom, and
+  // the last one also forms and searches a partial bottom row (~2 bands'
+  // time); so the first segment takes `top` rows more than the L of the
+  // middle ones and the last one the rest (1080p +-32: 10 + 6 x 8 + 9 rows,
+  // 12 bands each, against 13 for 8 x 9).
+  const int Sc = (S + 15) / 16, cus = bw_cu_count() * wgs_cu;
+  const int nfull = g->row0 + rows;  // (rows from row0: the job's full-height rows)
+  auto lo_b = [&](int br) { return std::max(16 * br - S, 0) >> 4; };
+  auto hi_b = [&](int br) { return std::min(16 * br + S, p.height - 16) >> 4; };
+  const int hbx = g->hb_row >= 0 ? 2 : 0;
+  auto seg_cost = [&](int r0, int r1) {  // bands of block rows [r0, r1) (+ the partial row's share)
+    return hi_b(r1 - 1) - lo_b(r0) + 1 + (r1 == nfull ? hbx : 0);
+  };
   const long per = (long)std::max(jobs, 1) * g->bw_strips;
-  for (int L = rows; L >= 4; L--) {
-    const long segs = (rows + L - 1) / L;
-    if ((rows + segs - 1) / segs != L) continue;  // even splits only
+  long best_t = 1L << 40;
+  int best_l = rows, best_top = 0, best_segs = 1;
+  for (int segs = 1; segs <= std::max(1, rows / 4); segs++) {
     const long rounds = (per * segs + cus - 1) / cus;
-    const long t = rounds * (L + extra);
-    if (t < best_t) {
-      best_t = (int)t;
-      best_l = L;
+    const int l0 = segs == 1 ? rows : std::max(1, (rows - 2 * Sc) / segs);
+    for (int L = l0; L <= l0 + 1 && L <= rows; L++) {
+      for (int top = 0; top <= (segs == 1 ? 0 : 2 * Sc + 2); top++) {
+        const int r0 = g->row0;
+        const int last0 = r0 + L + top + (segs - 2) * L;  // first row of the last segment
+        if (segs > 1 && (last0 >= nfull || L < 1)) continue;
+        int worst = seg_cost(r0, segs == 1 ? nfull : r0 + L + top);
+        if (segs > 2) worst = std::max(worst, seg_cost(r0 + L + top, r0 + 2 * L + top));
+        if (segs > 1) worst = std::max(worst, seg_cost(last0, nfull));
+        const long t = rounds * (worst + 2);
+        if (t < best_t) {
+          best_t = t;
+          best_l = segs == 1 ? rows : L;
+          best_top = segs == 1 ? 0 : top;
+          best_segs = segs;
+        }
+      }
     }
   }
-  if (tuning().bw_seg > 0) best_l = std::min(rows, tuning().bw_seg);
+  if (tuning().bw_seg > 0) {
+    best_l = std::min(rows, tuning().bw_seg);
+    best_top = 0;
+    best_segs = (rows + best_l - 1) / best_l;
+  }
   g->bw_seg_rows = best_l;
+  g->bw_seg_top = best_top;
   g->bw_abl = tuning().bw_abl;
-  g->bw_segs = (rows + best_l - 1) / best_l;
+  g->bw_segs = best_segs;
   // Launches of whole rounds of strips take the per-XCD tail split instead.
   g->bw_xt = 0;
   g->bw_cx = bw_cu_count() / 8;
   if (tuning().bw_xt != 0 && tuning().bw_seg == 0 && per >= cus && g->bw_cx > 0) {
     g->bw_xt = 1;
     g->bw_seg_rows = rows;
+    g->bw_seg_top = 0;
     g->bw_segs = 1;
   }
   g->lds = bw_lds_bytes(lp, pp, ns, nsw);

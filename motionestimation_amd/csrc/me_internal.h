@@ -7,6 +7,7 @@
 #include <stdarg.h>
 #include <stdint.h>
 
+#include <atomic>
 #include <condition_variable>
 #include <functional>
 #include <mutex>
@@ -184,8 +185,16 @@ struct me_ctx {
   bool comm_aborted = false;       // me_comm_check aborted rank_comm (failure detected)
   hipEvent_t comm_ev = nullptr;    // me_comm_check's marker on the checked stream
   me::Workers* pool = nullptr;     // me::workers(): persistent per-device host threads
+  // me_ctx_set_kernel_path: this context's kernel path code (me_tuning.h),
+  // -1 = the process-wide one; last_path[i]: ME_SEARCH_PATH_* of the latest
+  // search launched on devs[i] (me_ctx_last_search_path)
+  int path = -1;
+  std::vector<std::atomic<int>> last_path;
   char err[512] = {0};
 };
+
+#define ME_CTX_PATH_SCOPE(c, d) \
+  me::PathScope me_path_scope_((c)->path, &(c)->last_path[(size_t)(&(d) - (c)->devs.data())])
 
 #define HIPCHK(ctx, x)                                                                 \
   do {                                                                                 \

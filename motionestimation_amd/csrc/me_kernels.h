@@ -177,7 +177,8 @@ struct MfmaGeom {
   int bw_nsw, bw_pw;     // searcher and producer waves per workgroup
   int bw_cols;           // block columns per strip (bw_nsw / bw_wpc)
   int bw_strips;         // strips per job
-  int bw_seg_rows;       // block rows per workgroup
+  int bw_seg_rows;       // block rows per workgroup (segment)
+  int bw_seg_top;        // extra block rows of a job's first segment (it walks fewer bands)
   int bw_segs;           // segments per job
   int bw_xt;             // per-XCD tail split (bw_cx CUs per XCD): workgroup decode in bw_item()
   int bw_cx;
@@ -207,8 +208,9 @@ size_t merge_tiles_needed(const SearchArgs& p);
 bool mfma_disabled();
 
 hipError_t launch_search(const SearchArgs& p, hipStream_t stream, int* used_fast);
-// Records the kernel family of a search being launched (ME_SEARCH_PATH_*,
-// me_last_search_path).
+// Records the kernel family of a search being launched (ME_SEARCH_PATH_*):
+// process-wide (me_last_search_path) and, inside a PathScope, for the
+// context device the search runs on (me_ctx_last_search_path).
 void note_path(int path);
 int last_path();
 // Raise fn's dynamic-LDS limit to lds (> 64 KB) on the current device, once

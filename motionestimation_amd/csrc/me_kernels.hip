@@ -300,13 +300,22 @@ __device__ unsigned long long g_wstamps[8 << 14];
 // no literals: larger ones would each pin a VGPR and spill); invalid
 // candidates forced to sad 0xFFFF (> any valid SAD: B*B*255 <= 65280).
 // MASKJ = false on items whose whole dy range is valid (uniform per item).
-// min(a, b, c) as one v_min3_u32: written as min(min(..)) the compiler
-// reassociates the two key chains into trees of v_min + v_min3 (72 instead of
-// 52 instructions for the 104 keys of an 8x8 lane-task).
+// min(a, b, c) as one v_min3_u32 (ASM, K > 13: the 8x8 K = 26 lane-tasks):
+// written as min(min(..)) the compiler reassociates the two key chains into
+// trees of v_min + v_min3 (72 instead of 52 instructions for the 104 keys of
+// an 8x8 lane-task).  The K <= 13 instances keep plain C: the asm operands
+// pinned registers there and spilled 5 VGPRs of the 4K instance
+// <SAD, 16, 13, 272> (24 bytes per lane of scratch, 32 MiB of writes per
+// 16-frame launch; tests/test_kernel_resources.py guards it).
+template <bool ASM>
 __device__ __forceinline__ uint32_t min3u(uint32_t a, uint32_t b, uint32_t c) {
-  uint32_t r;
-  asm("v_min3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
+  if constexpr (ASM) {
+    uint32_t r;
+    asm("v_min3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+  } else {
+    return min(min(a, b), c);
+  }
 }
 
 template <int K, int J0, int J1, bool MASKJ>
@@ -328,8 +337,8 @@ __device__ __forceinline__ uint32_t lane_best_rows(const uint64_t (&acc)[K], uin
     const uint32_t k1 = (lo & 0xFFFF0000u) | (uint32_t)(5 * (j - J0) + 1);
     const uint32_t k2 = (hi << 16) | (uint32_t)(5 * (j - J0) + 2);
     const uint32_t k3 = (hi & 0xFFFF0000u) | (uint32_t)(5 * (j - J0) + 3);
-    b01 = min3u(b01, k0, k1);
-    b23 = min3u(b23, k2, k3);
+    b01 = min3u<(K > 13)>(b01, k0, k1);
+    b23 = min3u<(K > 13)>(b23, k2, k3);
   }
   return min(b01, b23);
 }
@@ -2028,10 +2037,6 @@ static hipError_t launch_valu(const SearchArgs& p, hipStream_t stream, int* used
   }
   return launch_items(p, stream, used_fast);
 }
-
-static std::atomic<int> g_last_path{0};
-void note_path(int path) { g_last_path.store(path, std::memory_order_relaxed); }
-int last_path() { return g_last_path.load(std::memory_order_relaxed); }
 
 hipError_t launch_jobs(const SearchArgs& base, const SearchJob* jobs, int n, hipStream_t stream) {
   hipError_t e;

@@ -9,6 +9,8 @@
 // with ME_HIP_LIB=libme_hip_tune.so.
 #pragma once
 
+#include <atomic>
+
 namespace me {
 
 struct Tuning {
@@ -48,15 +50,33 @@ struct Tuning {
                           // 64 no key epilogue, 128 no B-fragment reads in the tiles, 256 the
                           // MFMAs of ring slot 0 only;
                           // variants (results valid): 16 producer waves at raised priority,
-                          // 32 searcher waves at raised priority
+                          // 32 producer waves at raised priority for the first ring of bands
 };
 
 const Tuning& tuning();
 
-// Kernel path (me_set_kernel_path / ME_PATH): 0 automatic, 1 VALU kernels only,
-// 2 no block-major MFMA kernel, 3 block-major with S2 in the workgroup (lean).
-// Atomic: read by planner threads.
+// Kernel path: 0 automatic, 1 VALU kernels only, 2 the 4x4-block-tile MFMA
+// kernel for 16x16 SSD (no block-major kernel), 3 band-walk for every 16x16
+// SSD launch with S <= 64 (ME_PATH_MFMA_LEAN), 4 the prepass + block-major
+// pair (ME_PATH_MFMA_PREPASS).  The process-wide code (me_set_kernel_path /
+// ME_PATH) applies unless a PathScope of a context with its own path
+// (me_ctx_set_kernel_path) is active on the calling thread.  Atomic: read by
+// planner threads.
 int kernel_path();
 void set_kernel_path_code(int v);
+int path_code_of(int me_path_value);  // ME_PATH_* -> code above (-1 if invalid)
+
+// While alive on a thread: kernel_path() returns `path` when it is >= 0, and
+// note_path() also stores into *last (the context device's last search path).
+// Set around the planning and launch of a context's search (attach_scratch,
+// launch_ordered, launch_jobs_ordered); nests.
+struct PathScope {
+  PathScope(int path, std::atomic<int>* last);
+  ~PathScope();
+  PathScope(const PathScope&) = delete;
+  PathScope& operator=(const PathScope&) = delete;
+  int prev_path;
+  std::atomic<int>* prev_last;
+};
 
 }  // namespace me

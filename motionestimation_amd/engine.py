@@ -44,6 +44,9 @@ def plan_stripes(width: int, height: int, blk: int, span: int, shards: int) -> l
     return list(out)
 
 
+_PATH_CODES = {"auto": 0, "valu": 1, "tiles": 2, "lean": 3, "prepass": 4}
+
+
 def set_kernel_path(path: str) -> None:
     """'auto': 16x16 and 8x8 SSD on the matrix cores (i8 MFMA; 16x16 with
     S <= 64 on the band-walk kernel when a launch's strips fill the CUs, else
@@ -52,11 +55,9 @@ def set_kernel_path(path: str) -> None:
     MFMA kernel; 'lean': 16x16 SSD (S <= 64) on the band-walk kernel for every
     launch (no prepass planes, no scratch); 'prepass': 16x16 SSD on the S2
     prepass + block-major pair.  Process-wide; results are identical."""
-    codes = {"auto": _lib.ME_PATH_AUTO, "valu": _lib.ME_PATH_VALU, "tiles": _lib.ME_PATH_MFMA_TILES,
-             "lean": _lib.ME_PATH_MFMA_LEAN, "prepass": _lib.ME_PATH_MFMA_PREPASS}
-    if path not in codes:
+    if path not in _PATH_CODES:
         raise MEError(_lib.ME_EINVAL, f"unknown kernel path {path!r}")
-    _lib.lib().me_set_kernel_path(codes[path])
+    _lib.lib().me_set_kernel_path(_PATH_CODES[path])
 
 
 SEARCH_PATHS = {0: "none", 1: "valu", 2: "mfma_prepass", 3: "mfma_bandwalk", 4: "mfma_lean",
@@ -93,6 +94,19 @@ class Engine:
         self._h = h
         self.devices = list(devices) if devices else None
         self.comm_ranks = 0  # me_comm_init: size of this context's RCCL group
+
+    def set_kernel_path(self, path) -> None:
+        """This context's kernel path (me_ctx_set_kernel_path): one of
+        set_kernel_path()'s names, or None to follow the process-wide path."""
+        if path is not None and path not in _PATH_CODES:
+            raise MEError(_lib.ME_EINVAL, f"unknown kernel path {path!r}")
+        code = _lib.ME_PATH_PROCESS if path is None else _PATH_CODES[path]
+        check(_lib.lib().me_ctx_set_kernel_path(self._h, code), self._h)
+
+    def last_search_path(self, device_index: int = 0) -> str:
+        """The kernel family of this context's latest search on its device
+        `device_index` (me_ctx_last_search_path)."""
+        return SEARCH_PATHS.get(_lib.lib().me_ctx_last_search_path(self._h, device_index), "unknown")
 
     def close(self) -> None:
         if getattr(self, "_h", None):
@@ -388,6 +402,19 @@ class Graph:
             if s:
                 check(s, ctx)
         return run
+
+    def set_kernel_path(self, path) -> None:
+        """This context's kernel path (me_ctx_set_kernel_path): one of
+        set_kernel_path()'s names, or None to follow the process-wide path."""
+        if path is not None and path not in _PATH_CODES:
+            raise MEError(_lib.ME_EINVAL, f"unknown kernel path {path!r}")
+        code = _lib.ME_PATH_PROCESS if path is None else _PATH_CODES[path]
+        check(_lib.lib().me_ctx_set_kernel_path(self._h, code), self._h)
+
+    def last_search_path(self, device_index: int = 0) -> str:
+        """The kernel family of this context's latest search on its device
+        `device_index` (me_ctx_last_search_path)."""
+        return SEARCH_PATHS.get(_lib.lib().me_ctx_last_search_path(self._h, device_index), "unknown")
 
     def close(self) -> None:
         if getattr(self, "_h", None):

@@ -55,3 +55,18 @@ for k, nm in enumerate(names):
 for wv in range(nw):
     row = " ".join(f"{np.median(st[:, wv, k] / np.maximum(st[:, wv, 7], 1)):7.0f}" for k in range(1, 7))
     print(f"  wave {wv}: per iteration [entries fetch tiles end producer barrier] {row}")
+# producers (the last 4 waves): per-WG totals [slot wait, DMA wait, hb S2,
+# publish, production, hb search]
+print("  producer totals per workgroup (median cycles): slot-wait, DMA-wait, hb-S2, publish, production, hb-search")
+for wv in range(max(0, nw - 4), nw):
+    row = " ".join(f"{np.median(st[:, wv, k]):8.0f}" for k in (1, 2, 3, 4, 5, 6))
+    print(f"    wave {wv}: {row}")
+# per-workgroup lifetime (the longest wave) by bands walked: which segments
+# (top: fewer bands; bottom: + the partial row) end last
+life = tot.max(axis=1)
+print(f"  workgroup lifetime: median {np.median(life):.0f}  p90 {np.percentile(life, 90):.0f}  max {life.max():.0f}")
+for it in sorted(set(st[:, 0, 7].astype(int))):
+    sel = st[:, 0, 7].astype(int) == it
+    print(f"    {it:3d} bands: {sel.sum():4d} workgroups, lifetime median {np.median(life[sel]):.0f} max {life[sel].max():.0f}")
+    prod = " ".join(f"{np.median(st[sel][:, max(0, nw - 4):nw, k]):8.0f}" for k in (1, 2, 3, 4, 5, 6))
+    print(f"        producers (slot-wait, DMA-wait, hb-S2, publish, production, hb-search): {prod}")
