@@ -374,6 +374,50 @@ def ssd_beside(eng, ref_t, cur_t, blk, span, nb, cands_frame, dev, steps, pins, 
             "parity": par}
 
 
+def ssd_single(eng, ref_t, cur_t, blk, span, nb, cands_frame, dev, steps, pins, ramp_ms, config):
+    """The reference's own cost and call shape: ONE 16x16 SSD search per call
+    (the drop-in seam me_find_best_blocks / me_full_search replaces
+    src/cpu/main.c:144-158 with) on frame 0 of the step, on the path the
+    automatic planner picks for a single frame (`kernel_path`).  kernel_ms
+    from HIP events on the launch stream over `steps` back-to-back calls;
+    roofline against the dense i8 MFMA peak like ssd_mfma, with the PMC
+    traffic of the committed one-frame profile (`<config>_b16_s<S>_ssd_f1`,
+    tools/profile_all.sh) beside the algorithmic bytes.  The last call's
+    field is checked against the unmodified reference's pin of frame 0."""
+    import torch
+    import motionestimation_amd as me
+    h, w = ref_t.shape
+    mv = torch.empty((nb, 2), dtype=torch.int16, device=dev)
+    co = torch.empty(nb, dtype=torch.int32, device=dev)
+    run = lambda: eng.full_search_device(ref_t, cur_t, blk, span, "ssd", mv, co)  # noqa: E731
+    warm(run, ramp_ms)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(steps):
+        run()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / steps
+    kernel = me.last_search_path()
+    par = verify_fields(eng, batch_fields(mv, co, 1), None, None, w, h, blk, span, "ssd",
+                        pins[:1], dev, singles=False)
+    tops = 2.0 * exact_absdiffs(w, h, blk, span) / (ms / 1e3) / 1e12
+    traffic, traffic_search = load_traffic(f"{config}_b{blk}_s{span}_ssd_f1")
+    alg = 2 * w * h + 8 * nb
+    return {"value": cands_frame / (ms / 1e3), "unit": "candidates/s", "kernel_ms": ms,
+            "steps": steps, "kernel_path": kernel,
+            "workload": f"{w}x{h} Y, {blk}x{blk}, +-{span}, SSD (reference MSE argmin, bit-exact), "
+                        "one frame per call (me_full_search_device)",
+            "roofline": {"bound": "mfma", "achieved": tops, "peak": I8_PEAK_TOPS,
+                         "unit": "TFLOP/s", "frac": tops / I8_PEAK_TOPS,
+                         "traffic": traffic_search if traffic_search else traffic,
+                         "algorithmic_bytes": alg,
+                         "traffic_over_algorithmic": (traffic_search or traffic) / alg
+                         if (traffic_search or traffic) else None},
+            "parity": par}
+
+
 def ssim_beside(eng, ref_t, cur_t, blk, span, nb, dev, steps, ramp_ms):
     """The reference's SSIM search (src/common/ssim.c:44-108, ME_COST_SSIM) on
     frame 0 of the step (the committed golden ssim_synth1080p_b16_s32 is the
@@ -917,6 +961,9 @@ def launch_ranks(args):
     return 0
 
 
+T_START = time.perf_counter()
+
+
 def main():
     args = parse()
     if args.gpus < 1:
@@ -995,14 +1042,18 @@ def main():
         # Kernel duration: one HIP event pair on the stream the search is
         # launched on (torch's current stream) around the whole timed region,
         # / K (per-step event pairs would stretch the back-to-back launches).
+        t_timed = time.perf_counter()
         elapsed, kern_ms = timed(step, args.steps, args.warmup, world, ramp_ms=args.ramp_ms)
+        t_verify = time.perf_counter()
         # The timed step's own output (mv_t / cost_t hold the last step's
         # fields): device check, one-frame-per-call searches, and the pins of
         # this batch (rank 0: its frames are the pinned batch_frames).
         parity = verify_fields(eng, batch_fields(mv_t, cost_t, F), ref_t, cur_t, w, h, blk, span,
                                args.cost, pins if rank == 0 else [], dev)
         parity["ok"] = all_ranks_ok(parity["ok"], world)
+        t_done = time.perf_counter()
     else:
+        t_timed = time.perf_counter()
         ref, cur = synth.frame_pair(w, h, seed, sx, sy)
         frames = batch_frames(ref, cur, F)
         sr = StripeRun(eng, dev, world, rank, gloo, frames, blk, span, args.cost, args.graph,
@@ -1010,7 +1061,9 @@ def main():
         units_per_step = cands_frame * F
         elapsed, kern_ms = timed(sr.step, args.steps, args.warmup, world, ramp_ms=args.ramp_ms,
                                  drain=sr.drain)
+        t_verify = time.perf_counter()
         parity = stripe_parity(eng, sr, frames, dev, pins)
+        t_done = time.perf_counter()
 
     value = units_per_step * args.steps / elapsed
     # Roofline of the dominant kernel: algorithmic HBM bytes per
@@ -1101,30 +1154,52 @@ def main():
     # its own timed regions did; `parity` is false and the exit status
     # non-zero if any leg's fields differ or a kernel reported ME_EDEVICE.
     legs = {"timed_step": parity}
+    # wall seconds of every leg (stderr and the line's `wall_s`): what the
+    # driver's clock around this command covers besides the timed region
+    wall = {"startup": t_timed - T_START, "timed_step (warmup, ramp, K steps)": t_verify - t_timed,
+            "timed_step_parity": t_done - t_verify}
+
+    def leg_clock(name, t0):
+        wall[name] = time.perf_counter() - t0
+        print(f"bench.py: leg {name}: {wall[name]:.2f} s", file=sys.stderr, flush=True)
     if mode == "stripe":
         line["stripe_gather_parity"] = parity.get("batched_equal") == F if rank == 0 else None
         line["config"]["gather"] = sr.gather_impl()
     if rank == 0 and world == 1 and mode == "frames" and F > 1 and not args.no_single:
         # the same search one frame per launch (me_full_search_device), for
         # comparison: the batch's only difference is launches per frame
+        t0 = time.perf_counter()
         line["single_frame"] = single_frame(eng, ref_t[0], cur_t[0], blk, span, args.cost, nb,
                                             cands_frame, dev, min(args.steps * F, 100), pins,
                                             args.ramp_ms)
         legs["single_frame"] = line["single_frame"]["parity"]
+        leg_clock("single_frame", t0)
     if (rank == 0 and world == 1 and mode == "frames" and args.cost == "sad"
             and blk == 16 and not args.no_ssd):
+        t0 = time.perf_counter()
+        ssd_pins = load_pins(args.config, blk, span, "ssd")
         line["ssd_mfma"] = ssd_beside(eng, ref_t, cur_t, blk, span, nb, cands_frame, dev,
-                                      min(args.steps, 20), load_pins(args.config, blk, span, "ssd"),
-                                      args.ramp_ms, args.config)
+                                      min(args.steps, 20), ssd_pins, args.ramp_ms, args.config)
         legs["ssd_mfma"] = line["ssd_mfma"]["parity"]
+        leg_clock("ssd_mfma", t0)
+        t0 = time.perf_counter()
+        line["ssd_single_frame"] = ssd_single(eng, ref_t[0], cur_t[0], blk, span, nb, cands_frame,
+                                              dev, min(args.steps * F, 100), ssd_pins,
+                                              args.ramp_ms, args.config)
+        legs["ssd_single_frame"] = line["ssd_single_frame"]["parity"]
+        leg_clock("ssd_single_frame", t0)
     if (rank == 0 and world == 1 and mode == "frames" and args.config == "1080p"
             and args.cost == "sad" and not args.no_ssim):
+        t0 = time.perf_counter()
         line["ssim"] = ssim_beside(eng, ref_t[0], cur_t[0], blk, span, nb, dev,
                                    min(args.steps, 10), args.ramp_ms)
         legs["ssim"] = line["ssim"]["parity"]
+        leg_clock("ssim", t0)
     if rank == 0 and world == 1 and not args.no_cpu:
+        t0 = time.perf_counter()
         line["cpu_baseline"], field = cpu_baselines(ref, cur, blk, span, args.cost,
                                                     args.cpu_threads, cands_frame)
+        leg_clock("cpu_baseline", t0)
         if field is not None and mode == "frames":
             # the oracle's field of the CPU leg, run live on this box, against
             # frame 0 of the timed step (frame 0 = this ref/cur pair)
@@ -1135,21 +1210,28 @@ def main():
     if not args.no_4k and args.cost in ("sad", "ssd"):
         # BASELINE configs[3] (4K +-64), the config north_star's 8-GPU split is
         # quoted on, in stripe mode on the same ranks (at N = 1: the denominator)
+        t0 = time.perf_counter()
         rec4k = stripe_record(eng, dev, world, rank, gloo, "4k", args.cost,
                               min(args.steps, 20), min(args.warmup, 3), F, args.graph,
                               min(args.ramp_ms, 30.0), args.comm_timeout_ms)
         legs["stripe_4k"] = rec4k["parity"]
+        leg_clock("stripe_4k", t0)
         if rank == 0:
             line["stripe_4k"] = rec4k
     if rank == 0 and world == 1 and mode == "frames" and not args.no_stream:
         # per-frame kernel times (launch_ms covers a whole batched launch)
         one = line.get("single_frame", {}).get("kernel_ms", kern_ms / F)
+        t0 = time.perf_counter()
         line["host_stream"] = host_stream(eng, w, h, blk, span, args.cost, seed, sx, sy,
                                           one, kern_ms / F, cands_frame, args.ramp_ms)
         legs["host_stream"] = line["host_stream"]["parity"]
+        leg_clock("host_stream", t0)
     ok = all(leg["ok"] for leg in legs.values())
     line["parity"] = ok
     line["parity_legs"] = legs
+    wall["total"] = time.perf_counter() - T_START
+    line["wall_s"] = {k: round(v, 3) for k, v in wall.items()}
+    print(f"bench.py: wall {json.dumps(line['wall_s'])}", file=sys.stderr, flush=True)
     if rank == 0:
         print(json.dumps(line), file=json_out, flush=True)
     eng.close()

@@ -533,6 +533,7 @@ me_status multi_search(me_ctx* c, const uint8_t* ref, const uint8_t* cur, int wi
     me::Workers* pool = me::workers(c);
     if (!pool) return fail(c, ME_ENOMEM, "host worker threads");
     std::vector<me_ctx> errs(n);
+    for (me_ctx& e : errs) e.owner = c;
     std::vector<me_status> st(n, ME_OK);
     pool->run(n, [&](int i) {
       st[i] = stripe_upload_launch(&errs[i], c->devs[i], ref, cur, width, height, stride, blk,

@@ -85,6 +85,8 @@ constexpr int BW_PW = 4;             // producer waves per workgroup (one per SI
 // production, partial-row search, bands] (tools/bw_stamps.py).
 constexpr int BW_STW = 16;  // waves per workgroup slot
 __device__ unsigned long long g_bwstamps[BW_STW * 8 * 4096];
+// per workgroup and wave: s_memrealtime (100 MHz) at its start and end
+__device__ unsigned long long g_bwtimes[BW_STW * 2 * 4096];
 #define BW_T0() unsigned long long bw_t = __builtin_amdgcn_s_memtime()
 #define BW_ACC(k) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); bw_acc[k] += t_ - bw_t; bw_t = t_; } while (0)
 #else
@@ -93,6 +95,7 @@ __device__ unsigned long long g_bwstamps[BW_STW * 8 * 4096];
 #endif
 
 constexpr int BW_K = 8;              // band ring: the bands in flight (window + P0 plane each)
+
 constexpr int BW_WIN_ROWS = 31;      // window rows of a band: 16 b .. 16 b + 30
 
 // Producer -> searcher handshake per band slot (LDS): ready[k] = the band
@@ -167,11 +170,7 @@ __device__ __forceinline__ bool bw_wait(const SearchArgs& p, int lane, Pred ok) 
 // band times; its st segments ~ rows / st + that).  Launch order within an
 // XCD is blockIdx order, so the segments run last.
 struct BwItem {
-  // segment seg of item u: block rows [seg rows + (seg ? top : 0), + rows (+ top
-  // for seg 0)), clipped to the job's; the last one of an uneven plan takes
-  // the rest (last)
-  int u, seg, rows, top;
-  bool last;
+  int u, seg, rows;  // segment seg of item u: block rows [seg rows, + rows), clipped to the job's
 };
 __host__ __device__ inline void bw_xcd_split(int nx, int cx, int rows, int* main, int* kx, int* st,
                                              int* L) {
@@ -189,17 +188,17 @@ __device__ __forceinline__ BwItem bw_item(const MfmaGeom& g, int jobs) {
     const int per = g.bw_strips * g.bw_segs, j = lin / per;
     lin -= j * per;
     const int seg = lin / g.bw_strips;
-    return {j * g.bw_strips + lin - seg * g.bw_strips, seg, g.bw_seg_rows, g.bw_seg_top, seg == g.bw_segs - 1};
+    return {j * g.bw_strips + lin - seg * g.bw_strips, seg, g.bw_seg_rows};
   }
   const int b = (int)blockIdx.x, x = b & 7, m = b >> 3;
   const int U = jobs * g.bw_strips, q = U >> 3, rem = U & 7;
   const int nx = q + (x < rem ? 1 : 0), u0 = x * q + min(x, rem);
   int mainx, kx, st, L;
   bw_xcd_split(nx, g.bw_cx, g.bw_seg_rows, &mainx, &kx, &st, &L);
-  if (m < mainx) return {u0 + m, 0, g.bw_seg_rows, 0, true};
+  if (m < mainx) return {u0 + m, 0, g.bw_seg_rows};
   const int t = m - mainx;
-  if (t >= kx * st) return {-1, 0, 0, 0, false};
-  return {u0 + mainx + t % kx, t / kx, L, 0, false};
+  if (t >= kx * st) return {-1, 0, 0};
+  return {u0 + mainx + t % kx, t / kx, L};
 }
 
 template <int C, int NS, int LP, int NSW, int PW, bool ABL>
@@ -232,8 +231,8 @@ __global__ __launch_bounds__(64 * (NSW + PW), 4) void me_mfma_bw_kernel(SearchAr
     const int j = it.u / g.bw_strips;
     strip = it.u - j * g.bw_strips;
     mfma_job(jb, j, p, g);
-    r0 = g.row0 + it.seg * it.rows + (it.seg ? it.top : 0);
-    r1 = it.last ? g.row0 + g.nrows : min(g.row0 + (it.seg + 1) * it.rows + it.top, g.row0 + g.nrows);
+    r0 = g.row0 + it.seg * it.rows;
+    r1 = min(r0 + it.rows, g.row0 + g.nrows);
   }
   const int bc0 = strip * C, ncol = min(C, g.nbx - bc0);
   const int tc0 = max(16 * bc0 - S, 0) >> 4;  // first tile column of the strip window
@@ -331,9 +330,10 @@ __global__ __launch_bounds__(64 * (NSW + PW), 4) void me_mfma_bw_kernel(SearchAr
   // [O0, O1) (compile-time, at most 12): the rows of all the steps are read
   // first (one LDS latency).
   auto step_row = [](int o) { return o < 16 ? o : ((o - 16) & 1) ? ((o - 16) >> 1) + 16 : ((o - 16) >> 1); };
-  // Batches of steps are software-pipelined: the rows of batch i + 1 are
-  // read (ds_read2_b32) before batch i is computed, so an LDS round trip
-  // under the searchers' b128 traffic overlaps a batch of VALU work.
+  // A batch of steps [O0, O1) (compile-time, at most 12) reads the rows of
+  // all its steps first (one LDS round trip), then computes them.  (Reading
+  // batch i + 1 before computing batch i measured the same:
+  // profiles/r06g_bw_ab.jsonl.)
   auto load = [&](auto c0, auto c1, int k, uint32_t (&w0)[12], uint32_t (&w1)[12]) __attribute__((always_inline)) {
     constexpr int O0 = decltype(c0)::value, O1 = decltype(c1)::value;
     const uint32_t xa = (uint32_t)opaque((int)lds_addr(xw + k * WIN)) + 4u * (uint32_t)pg;
@@ -433,15 +433,15 @@ __global__ __launch_bounds__(64 * (NSW + PW), 4) void me_mfma_bw_kernel(SearchAr
     using I36 = std::integral_constant<int, 36>;
     using IE = std::integral_constant<int, BW_OPS>;
     xor_win(k);
-    uint32_t a0[12], a1[12], b0[12], b1[12];
-    load(I0{}, I12{}, k, a0, a1);
-    load(I12{}, I24{}, k, b0, b1);
-    steps(I0{}, I12{}, k, a0, a1);
-    load(I24{}, I36{}, k, a0, a1);
-    steps(I12{}, I24{}, k, b0, b1);
-    load(I36{}, IE{}, k, b0, b1);
-    steps(I24{}, I36{}, k, a0, a1);
-    steps(I36{}, IE{}, k, b0, b1);
+    uint32_t w0[12], w1[12];
+    load(I0{}, I12{}, k, w0, w1);
+    steps(I0{}, I12{}, k, w0, w1);
+    load(I12{}, I24{}, k, w0, w1);
+    steps(I12{}, I24{}, k, w0, w1);
+    load(I24{}, I36{}, k, w0, w1);
+    steps(I24{}, I36{}, k, w0, w1);
+    load(I36{}, IE{}, k, w0, w1);
+    steps(I36{}, IE{}, k, w0, w1);
   };
 
   // ================================ searchers
@@ -667,6 +667,7 @@ __global__ __launch_bounds__(64 * (NSW + PW), 4) void me_mfma_bw_kernel(SearchAr
 
 #ifdef ME_STAMPS
   unsigned long long bw_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const unsigned long long bw_rt0 = __builtin_amdgcn_s_memrealtime();
 #endif
   BW_T0();
   if (tid < nkeys) keys[tid] = ~0ull;
@@ -699,27 +700,20 @@ __global__ __launch_bounds__(64 * (NSW + PW), 4) void me_mfma_bw_kernel(SearchAr
     // (tuning build: bit 16 raises the producers' issue priority for the
     // whole walk, bit 32 for the first ring of bands only)
     if (ABL && (g.bw_abl & 48)) __builtin_amdgcn_s_setprio(2);
-    // Band m + PW's window is DMA'd before band m is produced when its slot
-    // is free already (the DMA then lands during the production), otherwise
-    // right after band m is published: a producer never waits for the
-    // searchers before producing a band whose window it has (waiting there
-    // held every producer to the searchers' pace, one band behind: the
-    // slot-wait was ~20 % of a single-frame segment).
-    auto slot_free = [&](int m) {
-      return m - BW_K < bfirst ||
-             __hip_atomic_load(&ctl->done[m % BW_K], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= nact;
-    };
+    // Band m + PW's window is DMA'd (its slot released by every searcher
+    // first) before band m is produced, so the DMA latency hides behind one
+    // band's production.  (Claiming it only when already free, else after band
+    // m is published, measured the same: profiles/r06g_bw_ab.jsonl.)
     bool ok = bfirst + pw > blast_p || claim(bfirst + pw);
 #pragma unroll 1
     for (int m = bfirst + pw; ok && m <= blast_p; m += PW) {
       const int k = m % BW_K;
       if (ABL && (g.bw_abl & 32) && m >= bfirst + BW_K) __builtin_amdgcn_s_setprio(0);
       const bool next = m + PW <= blast_p;
-      const bool ahead = next && __builtin_amdgcn_readfirstlane(slot_free(m + PW) ? 1 : 0);
-      if (ahead) ok = claim(m + PW);  // (free: no wait)
+      if (next) ok = claim(m + PW);
       BW_ACC(1);
       // band m's window landed (band m + PW's DMA may still be in flight)
-      if (ahead)
+      if (next)
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DMA_N) : "memory");
       else
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -737,8 +731,6 @@ __global__ __launch_bounds__(64 * (NSW + PW), 4) void me_mfma_bw_kernel(SearchAr
         if (lane == 0) __hip_atomic_store(&ctl->hbready[m - lo_h], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         BW_ACC(3);  // (stamps, producers: the partial row's S2)
       }
-      if (next && !ahead) ok = claim(m + PW);
-      BW_ACC(1);
     }
   } else {
    if (hascol) {
@@ -892,6 +884,8 @@ __global__ __launch_bounds__(64 * (NSW + PW), 4) void me_mfma_bw_kernel(SearchAr
   if (lane == 0 && blockIdx.x < 4096) {
     bw_acc[7] = (unsigned long long)(blast - bfirst + 1);
     for (int k = 0; k < 8; k++) g_bwstamps[(blockIdx.x * BW_STW + wave) * 8 + k] = bw_acc[k];
+    g_bwtimes[(blockIdx.x * BW_STW + wave) * 2] = bw_rt0;
+    g_bwtimes[(blockIdx.x * BW_STW + wave) * 2 + 1] = __builtin_amdgcn_s_memrealtime();
   }
 #endif
 }
@@ -953,51 +947,36 @@ bool plan_bw(const SearchArgs& p, MfmaGeom* g, int jobs) {
   g->bw_strips = (g->nbx + C - 1) / C;
   // Segments: rounds of resident workgroups x (the most bands one segment
   // walks + ~2 bands of prologue), the smallest.  A segment of rows [r0, r1)
-  // walks bands lo(r0) .. hi(r1 - 1), 2 ceil(S/16) more than its rows in the
-  // middle of the frame but only ceil(S/16) more at the top and bottom, and
-  // the last one also forms and searches a partial bottom row (~2 bands'
-  // time); so the first segment takes `top` rows more than the L of the
-  // middle ones and the last one the rest (1080p +-32: 10 + 6 x 8 + 9 rows,
-  // 12 bands each, against 13 for 8 x 9).
-  const int Sc = (S + 15) / 16, cus = bw_cu_count() * wgs_cu;
+  // walks bands lo(r0) .. hi(r1 - 1); even splits, the last segment the
+  // rest.  (Uneven splits -- a longer first segment, which walks ceil(S/16)
+  // fewer bands, the partial row's segment shorter -- measured 1.5 % slower
+  // at 1080p: profiles/r06g_bw_ab.jsonl.)
+  const int cus = bw_cu_count() * wgs_cu;
   const int nfull = g->row0 + rows;  // (rows from row0: the job's full-height rows)
   auto lo_b = [&](int br) { return std::max(16 * br - S, 0) >> 4; };
   auto hi_b = [&](int br) { return std::min(16 * br + S, p.height - 16) >> 4; };
-  const int hbx = g->hb_row >= 0 ? 2 : 0;
-  auto seg_cost = [&](int r0, int r1) {  // bands of block rows [r0, r1) (+ the partial row's share)
-    return hi_b(r1 - 1) - lo_b(r0) + 1 + (r1 == nfull ? hbx : 0);
-  };
   const long per = (long)std::max(jobs, 1) * g->bw_strips;
   long best_t = 1L << 40;
-  int best_l = rows, best_top = 0, best_segs = 1;
+  int best_l = rows, best_segs = 1;
   for (int segs = 1; segs <= std::max(1, rows / 4); segs++) {
+    const int L = (rows + segs - 1) / segs;
+    if ((rows + L - 1) / L != segs) continue;  // (an empty last segment)
     const long rounds = (per * segs + cus - 1) / cus;
-    const int l0 = segs == 1 ? rows : std::max(1, (rows - 2 * Sc) / segs);
-    for (int L = l0; L <= l0 + 1 && L <= rows; L++) {
-      for (int top = 0; top <= (segs == 1 ? 0 : 2 * Sc + 2); top++) {
-        const int r0 = g->row0;
-        const int last0 = r0 + L + top + (segs - 2) * L;  // first row of the last segment
-        if (segs > 1 && (last0 >= nfull || L < 1)) continue;
-        int worst = seg_cost(r0, segs == 1 ? nfull : r0 + L + top);
-        if (segs > 2) worst = std::max(worst, seg_cost(r0 + L + top, r0 + 2 * L + top));
-        if (segs > 1) worst = std::max(worst, seg_cost(last0, nfull));
-        const long t = rounds * (worst + 2);
-        if (t < best_t) {
-          best_t = t;
-          best_l = segs == 1 ? rows : L;
-          best_top = segs == 1 ? 0 : top;
-          best_segs = segs;
-        }
-      }
+    int worst = 0;  // bands of the longest segment
+    for (int r0 = g->row0; r0 < nfull; r0 += L)
+      worst = std::max(worst, hi_b(std::min(r0 + L, nfull) - 1) - lo_b(r0) + 1);
+    const long t = rounds * (worst + 2);
+    if (t < best_t) {
+      best_t = t;
+      best_l = L;
+      best_segs = segs;
     }
   }
   if (tuning().bw_seg > 0) {
     best_l = std::min(rows, tuning().bw_seg);
-    best_top = 0;
     best_segs = (rows + best_l - 1) / best_l;
   }
   g->bw_seg_rows = best_l;
-  g->bw_seg_top = best_top;
   g->bw_abl = tuning().bw_abl;
   g->bw_segs = best_segs;
   // Launches of whole rounds of strips take the per-XCD tail split instead.
@@ -1006,7 +985,6 @@ bool plan_bw(const SearchArgs& p, MfmaGeom* g, int jobs) {
   if (tuning().bw_xt != 0 && tuning().bw_seg == 0 && per >= cus && g->bw_cx > 0) {
     g->bw_xt = 1;
     g->bw_seg_rows = rows;
-    g->bw_seg_top = 0;
     g->bw_segs = 1;
   }
   g->lds = bw_lds_bytes(lp, pp, ns, nsw);
@@ -1026,6 +1004,10 @@ bool plan_bw(const SearchArgs& p, MfmaGeom* g, int jobs) {
   }
   g->bw = 1;
   return true;
+}
+
+bool bw_one_round(const MfmaGeom& g, int jobs) {
+  return (long)std::max(jobs, 1) * g.bw_strips * g.bw_segs <= (long)bw_cu_count();
 }
 
 hipError_t launch_bw(const SearchArgs& p, const MfmaGeom& g0, const MfmaJobs& jb0, hipStream_t stream) {
@@ -1068,6 +1050,11 @@ hipError_t launch_bw(const SearchArgs& p, const MfmaGeom& g0, const MfmaJobs& jb
 }  // namespace me
 
 #ifdef ME_STAMPS
+extern "C" int me_debug_bw_times(unsigned long long* out, int n_words) {
+  if (n_words > me::BW_STW * 2 * 4096) n_words = me::BW_STW * 2 * 4096;
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(me::g_bwtimes), (size_t)n_words * 8, 0,
+                                  hipMemcpyDeviceToHost);
+}
 extern "C" int me_debug_bw_stamps(unsigned long long* out, int n_words) {
   if (n_words > me::BW_STW * 8 * 4096) n_words = me::BW_STW * 8 * 4096;
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(me::g_bwstamps), (size_t)n_words * 8, 0,

@@ -190,11 +190,25 @@ struct me_ctx {
   // search launched on devs[i] (me_ctx_last_search_path)
   int path = -1;
   std::vector<std::atomic<int>> last_path;
+  // A per-device error context of a multi-device call (its worker's failure
+  // message) points at the context the call is for: the kernel path and the
+  // last-path slots are that context's.
+  me_ctx* owner = nullptr;
   char err[512] = {0};
 };
 
-#define ME_CTX_PATH_SCOPE(c, d) \
-  me::PathScope me_path_scope_((c)->path, &(c)->last_path[(size_t)(&(d) - (c)->devs.data())])
+namespace me {
+// The last-path slot of device d of the context c serves (nullptr if d is not
+// one of its devices).
+inline std::atomic<int>* ctx_last_slot(me_ctx* c, Dev& d) {
+  const ptrdiff_t i = &d - c->devs.data();
+  return i >= 0 && (size_t)i < c->last_path.size() ? &c->last_path[(size_t)i] : nullptr;
+}
+}  // namespace me
+
+#define ME_CTX_PATH_SCOPE(c, d)                                  \
+  me_ctx* const me_path_ctx_ = (c)->owner ? (c)->owner : (c);    \
+  me::PathScope me_path_scope_(me_path_ctx_->path, me::ctx_last_slot(me_path_ctx_, (d)))
 
 #define HIPCHK(ctx, x)                                                                 \
   do {                                                                                 \

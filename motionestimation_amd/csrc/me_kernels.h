@@ -178,7 +178,6 @@ struct MfmaGeom {
   int bw_cols;           // block columns per strip (bw_nsw / bw_wpc)
   int bw_strips;         // strips per job
   int bw_seg_rows;       // block rows per workgroup (segment)
-  int bw_seg_top;        // extra block rows of a job's first segment (it walks fewer bands)
   int bw_segs;           // segments per job
   int bw_xt;             // per-XCD tail split (bw_cx CUs per XCD): workgroup decode in bw_item()
   int bw_cx;
@@ -201,6 +200,9 @@ bool launch_mfma_jobs(const SearchArgs& base, const SearchJob* jobs, int n, hipS
 // Band-walk kernel (me_band.hip): plan the full-height rows of p into g (g's
 // common fields already set by plan_mfma_ssd), and launch every job of jb.
 bool plan_bw(const SearchArgs& p, MfmaGeom* g, int jobs);
+// The band-walk plan g (plan_bw) for `jobs` jobs per launch runs in one
+// round of workgroups (every segment of every strip resident at once).
+bool bw_one_round(const MfmaGeom& g, int jobs);
 hipError_t launch_bw(const SearchArgs& p, const MfmaGeom& g, const MfmaJobs& jb, hipStream_t stream);
 // Tiles of cross-workgroup merge buffers (mkeys: 16 u64 keys each, ~0; mcnt:
 // one u32 counter each, 0) the search of p needs (the MFMA SSD kernels).

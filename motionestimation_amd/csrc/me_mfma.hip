@@ -1748,18 +1748,22 @@ static bool plan_mfma_ssd8(const SearchArgs& p, MfmaGeom* g);
 static bool bm_auto(const SearchArgs& p) { return p.range <= 192; }
 
 // The automatic path's choice for `jobs` frames of p's shape per launch:
-// the band-walk kernel (lean: no prepass planes, ~1.1x the algorithmic HBM
-// bytes) when the launch's strips fill the CUs without splitting block rows
-// into segments (each segment re-forms 2 ceil(S/16) bands around it; a single
-// 1080p frame would be 8 segments of 9 rows: 68.8 us against 36.7 on the
-// prepass pair, 16 frames per launch 24.5 against 24.4: profiles/r05za_*).
+// the band-walk kernel (lean: no prepass planes, ~1.0-1.3x the algorithmic
+// HBM bytes against ~7x) when its plan runs in one round of workgroups or
+// without splitting block rows into segments (each segment re-forms
+// 2 ceil(S/16) bands around it).  A single 1080p frame is 8 segments of 9
+// rows in one round: 37.5 against 37.8-38.8 us per call on the prepass pair;
+// 4K +-64 (2 segments of 68 rows): 265.9 against 254 us, the price of ~18
+// against ~122 MB of HBM traffic per search (profiles/r06h_ssd_ab.jsonl, one
+// box).  The round-5 figure of 68.8 us was the partial bottom row's second
+// launch, now searched inside the walk.
 // ME_PATH_MFMA_LEAN (force) takes the band-walk kernel whenever it applies.
 // g holds the block-major plan on entry and the band-walk plan on success.
 static bool use_bw(const SearchArgs& p, MfmaGeom* g, int jobs, bool force = false) {
   if (!g->bm) return false;
   MfmaGeom t = *g;
   t.bmv = 0;
-  if (!plan_bw(p, &t, jobs) || (!force && t.bw_segs != 1)) return false;
+  if (!plan_bw(p, &t, jobs) || (!force && t.bw_segs != 1 && !bw_one_round(t, jobs))) return false;
   *g = t;
   g->bmv_r = 1;
   g->scratch_bytes = 0;
@@ -2051,10 +2055,16 @@ static int batch_jobs(const MfmaGeom& g, int n) {
 size_t mfma_batch_scratch(const SearchArgs& p, int n) {
   MfmaGeom g;
   if (!plan_mfma_ssd(p, &g) || g.bmv || g.bw) return 0;
+  // launch_mfma_jobs runs the batch job by job, each on its own single-frame
+  // plan, when a job has a partial right column or its planes are not
+  // aligned like job 0's: the scratch then has to hold one job's prepass
+  // planes (a batch that fell back with none ran on the VALU kernels)
+  const size_t one = g.scratch_bytes;
+  if (g.nbx < p.nbx) return one;
   if (n >= 2 && kernel_path() == 0 && tuning().mfma_batch != 0 && use_bw(p, &g, n < MAX_JOBS ? n : MAX_JOBS))
-    return 0;  // the batch runs on the band-walk kernel
+    return one;  // the batch runs on the band-walk kernel (no planes) unless it falls back
   const int m = batch_jobs(g, n);
-  return m ? (size_t)m * batch_stride(g) : g.scratch_bytes;
+  return m ? ((size_t)m * batch_stride(g) > one ? (size_t)m * batch_stride(g) : one) : one;
 }
 
 bool launch_mfma_jobs(const SearchArgs& base, const SearchJob* jobs, int n, hipStream_t stream,

@@ -177,14 +177,19 @@ me_status run_pairs(me_ctx* c, Dev& d, const Job& j, int p0, int p1) {
   if ((s = grow(c, (void**)&d.pair_out, &d.pair_out_cap, np * nb * 8)) != ME_OK) return s;
   int16_t* out_mv = reinterpret_cast<int16_t*>(d.pair_out);
   uint32_t* out_cost = reinterpret_cast<uint32_t*>(d.pair_out + np * nb * 4);
-  // Pinned bounce buffer for the records: one region of G pairs per batch
-  // event, indexed by batch mod kEvRing (drain() keeps fewer than kEvRing
-  // batches between download and drain, so a region is free again when its
-  // batch index comes round): at most kEvRing * G pairs pinned, whatever the
-  // length of the pair list.
+  // Pinned bounce buffer for the records: one region of G pairs per batch,
+  // indexed by batch mod the region count: one region per batch of this
+  // call (the ramp's batches counted exactly) up to kEvRing, and drain()
+  // keeps fewer than kEvRing batches between download and drain, so a region
+  // is free again when its batch index comes round: at most kEvRing * G
+  // pairs pinned, whatever the length of the pair list.  (Round 5 sized it
+  // ceil(np / G) + 4, below the ramp's batch count for a large G.)
   const int G = tuning().stream_batch > 0 ? tuning().stream_batch : kPairBatch;
   const size_t region = (size_t)G * nb * 8;  // [G * nb mv (4 B)][G * nb cost (4 B)]
-  const size_t bneed = region * (size_t)std::min<size_t>(kEvRing, (np + G - 1) / G + 4);
+  size_t nbatches = 0;
+  for (size_t n0 = 0, gb = 1; n0 < np; n0 += gb, gb = std::min<size_t>(gb + std::max<size_t>(1, gb / 2), G))
+    nbatches++;
+  const size_t bneed = region * std::min<size_t>(kEvRing, nbatches);
   if (d.bounce_cap < bneed) {
     if (d.bounce) (void)hipHostFree(d.bounce);
     d.bounce = nullptr;
@@ -435,6 +440,7 @@ me_status me_search_pairs(me_ctx* c, const uint8_t* const* frames, int n_frames,
   me::Workers* pool = me::workers(c);
   if (!pool) return me::fail(c, ME_ENOMEM, "host worker threads");
   std::vector<me_ctx> errs(nd);
+  for (me_ctx& e : errs) e.owner = c;
   std::vector<me_status> st(nd, ME_OK);
   pool->run(nd, [&](int i) {
     const int p0 = (int)((long)n_pairs * i / nd), p1 = (int)((long)n_pairs * (i + 1) / nd);

@@ -93,3 +93,22 @@ def test_ctx_path_argument_checks():
         assert _lib.lib().me_ctx_set_kernel_path(eng._h, 99) == _lib.ME_EINVAL
         assert _lib.lib().me_ctx_last_search_path(eng._h, 5) == -1
         assert _lib.lib().me_ctx_last_search_path(None, 0) == -1
+
+
+def test_multi_device_context_path_on_worker_threads():
+    """A context over the device list [0, 0] runs me_search_pairs on one host
+    worker per context device; the workers plan with the context's own path
+    and record it per device (round 6: their per-device error contexts first
+    indexed the wrong context's slots and crashed)."""
+    frames = [_pair(s, 208, 256)[0] for s in range(5)]
+    pairs = [(0, 1), (1, 2), (2, 3), (3, 4), (4, 0), (1, 3)]
+    me.set_kernel_path("auto")
+    with me.Engine(devices=[0, 0]) as eng:
+        eng.set_kernel_path("prepass")
+        mv, c = eng.search_pairs(frames, pairs, 16, 16, "ssd")
+        assert eng.last_search_path(0) == "mfma_prepass", eng.last_search_path(0)
+        assert eng.last_search_path(1) == "mfma_prepass", eng.last_search_path(1)
+        for i, (a, b) in enumerate(pairs):
+            omv, oc, _ = O.full_search(frames[a], frames[b], 16, 16, "ssd", threads=NT)
+            np.testing.assert_array_equal(mv[i], omv, err_msg=f"pair {i}")
+            np.testing.assert_array_equal(c[i], oc, err_msg=f"pair {i}")

@@ -318,24 +318,27 @@ def test_mfma_batch_mixed_alignment(engine):
 
 
 @pytest.mark.parametrize("shape,span", [((720, 1280), 32), ((544, 960), 16), ((368, 656), 64),
-                                        ((1080, 1920), 32)])
+                                        ((1080, 1920), 32), ((376, 656), 64), ((1080, 1920), 48)])
 def test_band_walk_segments_and_batches(engine, ssd_path, shape, span):
     """The band-walk kernel splits a frame into segments of block rows when
     its strips alone do not fill the CUs (single frames) and walks whole
     strips in batches: one frame, and the same frame in a batch of 6 with
-    other frames, against the oracle (partial bottom rows: 368 = 23 x 16,
-    1080 = 67 x 16 + 8, handed to the lean kernel)."""
+    other frames, against the oracle.  Partial bottom block rows: 1080 =
+    67 x 16 + 8 (S 32: searched inside the walk on its own S2 planes; S 48:
+    its planes do not fit beside the ring, so a second launch of the lean
+    kernel me_mfma_bmv_kernel searches it) and 376 = 23 x 16 + 8 at S 64 (the
+    same second launch); 368 = 23 x 16 has none."""
     import torch
-    if ssd_path != "lean":
-        pytest.skip("band-walk geometry: the lean path forces the band-walk kernel")
+    if ssd_path == "prepass":
+        pytest.skip("band-walk geometry: the auto and lean paths run the band-walk kernel")
     h, w = shape
     rng = np.random.default_rng(h + span)
     pairs = [_pair(rng, h, w, dx=int(rng.integers(-5, 6)), dy=int(rng.integers(-5, 6))) for _ in range(6)]
     ref, cur = pairs[0]
     _check(engine, ref, cur, span, f"{h}x{w} S{span} single")
-    # the lean path runs the band-walk kernel on a single frame too (round 5:
-    # a missing scratch check had sent band-walk searches to the VALU
-    # kernels, correct but 3x slower)
+    # the auto and lean paths run the band-walk kernel on a single frame too
+    # (round 5: a missing scratch check had sent band-walk searches to the
+    # VALU kernels, correct but 3x slower)
     engine.full_search(ref, cur, 16, span, "ssd")
     assert me.last_search_path() == "mfma_bandwalk", me.last_search_path()
     dev = torch.device("cuda", 0)
@@ -421,13 +424,13 @@ def test_band_walk_forced_segment_rows(tmp_path, seg):
     assert "segments ok" in r.stdout
 
 
-@pytest.mark.parametrize("path,want", [("auto", "mfma_prepass"), ("prepass", "mfma_prepass"),
+@pytest.mark.parametrize("path,want", [("auto", "mfma_bandwalk"), ("prepass", "mfma_prepass"),
                                        ("lean", "mfma_bandwalk"), ("tiles", "mfma_tiles"), ("valu", "valu")])
 def test_kernel_path_reported(engine, path, want):
     """me_last_search_path names the kernel family each me_set_kernel_path
     value runs for a 16x16 +-32 SSD search of one small frame (on the
-    automatic path its strips cannot fill the CUs: the prepass pair); SAD runs
-    the VALU kernels on every path."""
+    automatic path the band-walk kernel: its segments run in one round of
+    workgroups); SAD runs the VALU kernels on every path."""
     rng = np.random.default_rng(11)
     ref, cur = _pair(rng, 256, 320, dx=2, dy=-1)
     try:
@@ -441,3 +444,34 @@ def test_kernel_path_reported(engine, path, want):
         assert me.last_search_path() == "valu"
     finally:
         me.set_kernel_path("auto")
+
+
+def test_batched_ssd_partial_right_column_stays_on_mfma(engine, ssd_path):
+    """A batch of 16x16 SSD frames whose width is not a multiple of 16 (854 =
+    53 x 16 + 6, rows at a 16-byte pitch of 864): launch_mfma_jobs runs it job
+    by job (the partial right column goes to the VALU kernels per frame), and
+    the context scratch must hold one job's prepass planes for the prepass
+    path -- round 5 sized it for the band-walk batch (none) and the fallback
+    silently ran every full column on the VALU kernels.  The full
+    columns stay on the matrix cores and the fields equal the oracle's."""
+    import torch
+    h, w, pitch, span, F = 344, 854, 864, 32, 4
+    rng = np.random.default_rng(854)
+    pairs = [_pair(rng, h, w, dx=int(rng.integers(-4, 5)), dy=int(rng.integers(-4, 5))) for _ in range(F)]
+    dev = torch.device("cuda", 0)
+    nb = me.num_blocks(w, h, 16)
+    pad = lambda a: np.pad(a, ((0, 0), (0, pitch - w)))  # noqa: E731
+    rt = torch.from_numpy(np.stack([pad(r) for r, _ in pairs])).to(dev)
+    ct = torch.from_numpy(np.stack([pad(c) for _, c in pairs])).to(dev)
+    mv = torch.empty((F * nb, 2), dtype=torch.int16, device=dev)
+    co = torch.empty(F * nb, dtype=torch.int32, device=dev)
+    engine.search_batch_device(rt, 0, ct, 0, w, h, 16, span, "ssd", 0, (h + 15) // 16, mv, co)
+    torch.cuda.synchronize()
+    engine.device_check()
+    want = {"auto": "mfma_bandwalk", "lean": "mfma_bandwalk", "prepass": "mfma_prepass"}[ssd_path]
+    assert engine.last_search_path() == want, (ssd_path, engine.last_search_path())
+    mv, co = mv.cpu().numpy().reshape(F, nb, 2), co.cpu().numpy().view(np.uint32).reshape(F, nb)
+    for f, (r, c) in enumerate(pairs):
+        omv, oc, _ = O.full_search(r, c, 16, span, "ssd", threads=NT)
+        np.testing.assert_array_equal(mv[f], omv, err_msg=f"frame {f}")
+        np.testing.assert_array_equal(co[f], oc, err_msg=f"frame {f}")

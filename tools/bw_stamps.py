@@ -70,3 +70,15 @@ for it in sorted(set(st[:, 0, 7].astype(int))):
     print(f"    {it:3d} bands: {sel.sum():4d} workgroups, lifetime median {np.median(life[sel]):.0f} max {life[sel].max():.0f}")
     prod = " ".join(f"{np.median(st[sel][:, max(0, nw - 4):nw, k]):8.0f}" for k in (1, 2, 3, 4, 5, 6))
     print(f"        producers (slot-wait, DMA-wait, hb-S2, publish, production, hb-search): {prod}")
+
+# absolute times (s_memrealtime, 100 MHz) of the last launch: workgroup start
+# stagger and end spread, relative to the first workgroup's start
+L.me_debug_bw_times.argtypes = [ctypes.c_void_p, ctypes.c_int]
+tb = np.zeros(NW * 2 * 4096, np.uint64)
+L.me_debug_bw_times(tb.ctypes.data, tb.size)
+tt = tb.reshape(4096, NW, 2)[used][:, :nw].astype(np.float64)
+t0 = tt[:, :, 0].min()
+starts = (tt[:, :, 0].min(axis=1) - t0) / 100.0  # us
+ends = (tt[:, :, 1].max(axis=1) - t0) / 100.0
+print(f"  workgroup start (us after the first): median {np.median(starts):.2f} p90 {np.percentile(starts, 90):.2f} max {starts.max():.2f}")
+print(f"  workgroup end   (us after the first start): min {ends.min():.2f} median {np.median(ends):.2f} p90 {np.percentile(ends, 90):.2f} max {ends.max():.2f}")
