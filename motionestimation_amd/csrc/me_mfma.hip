@@ -859,7 +859,10 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd8_kernel(SearchArgs p, M
       load_row(rw[0], std::integral_constant<int, 0>{});
       load_row(rw[1], std::integral_constant<int, 1>{});
       sv[0] = *reinterpret_cast<lds_i32*>((uintptr_t)sp);
-      // fully unrolled: the 3-row ring index t % 3 must be static
+      // fully unrolled: the 3-row ring index t % 3 must be static.  (Issuing
+      // step t's MFMA before step t - 1's keys, and the position term
+      // precomputed in the S2 table, measured the same or slower:
+      // profiles/r06k_ssd8_ab.jsonl)
       sfor<0, L>([&](auto TT) {
         constexpr int t = decltype(TT)::value;
         // rows t+2h in rw[t % 3], t+2h+1 in rw[(t+1) % 3]; prefetch t+2h+2
