@@ -20,8 +20,9 @@
 // block_cost carries the float bits of the best score.
 //
 // One workgroup per block, SSIM_Q adjacent candidates per lane per step; the
-// block and its window are staged in LDS when they fit.  Float-chain bound,
-// not a hot path of the headline metric.
+// block and its window are staged in LDS when they fit.  Float-chain bound
+// (packed fp32: one v_pk_add + one v_pk_fma per two candidate pixels), not a
+// hot path of the headline metric.
 //
 // Patch statistics prepass (round 3): a ref patch's mean and stddev depend on
 // its position only, yet every block whose window covers the position
@@ -34,7 +35,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "me_kernels.h"
+#include "me_mfma_util.h"
 
 namespace me {
 
@@ -43,7 +47,10 @@ namespace {
 constexpr int SSIM_THREADS = 256;
 constexpr int SSIM_Q = 4;   // adjacent candidates per lane (in-kernel statistics)
 constexpr int SSIM_QP = 8;  // ... with the statistics plane (one cross chain each)
-constexpr int SSIM_Q16 = 12; // ... 16 x 16 blocks (1080p +-32: 6: 1.27 ms, 8: 0.88, 12: 0.72, 16: 0.81; profiles/r03bc_*, r03bd_*)
+// ... 16 x 16 blocks with the statistics plane on the float path (1080p +-32:
+// 6: 1.27 ms, 8: 0.88, 12: 0.72, 16: 0.81; profiles/r03bc_*, r03bd_*; 13 and
+// workgroups sized to one round of lane-tasks: slower, profiles/r06k_*)
+constexpr int SSIM_Q16 = 12;
 // LDS bytes past the window: the last row's last candidate group reads up to
 // SSIM_QP (8-candidate groups) or SSIM_Q16 - 1 (16x16 register rows) bytes past it
 constexpr int SSIM_PAD = SSIM_QP > SSIM_Q16 - 1 ? SSIM_QP : SSIM_Q16 - 1;
@@ -76,6 +83,23 @@ __device__ __forceinline__ void patch_stats(const uint8_t* p, int pitch, int w, 
 
 __device__ __forceinline__ float sqrt_via_double(float v) {
   return __double2float_rn(__dsqrt_rn((double)v));
+}
+
+// ssim.c:53-56 for one candidate: the ref patch's mean m and stddev sr, the
+// cross variance cvk, the current block's mean mp and stddev sp -> the key
+// (0x7FFFFFFF - bits(score)) << 32 | (dy, dx), or ~0 for a score <= 0.
+__device__ __forceinline__ uint64_t ssim_key(float m, float sr, float cvk, float mp, float sp,
+                                             int dx, int dy) {
+  const float C1 = 0.01f, C2 = 0.09f, C3 = 0.045f;  // ssim.c:48
+  const float lum = __fdiv_rn(__fadd_rn(__fmul_rn(__fmul_rn(2.f, m), mp), C1),
+                              __fadd_rn(__fadd_rn(__fmul_rn(m, m), __fmul_rn(mp, mp)), C1));
+  const float con = __fdiv_rn(__fadd_rn(__fmul_rn(__fmul_rn(2.f, sr), sp), C2),
+                              __fadd_rn(__fadd_rn(__fmul_rn(sr, sr), __fmul_rn(sp, sp)), C2));
+  const float str = __fdiv_rn(__fadd_rn(cvk, C3), __fadd_rn(__fmul_rn(sr, sp), C3));
+  const float score = __fmul_rn(__fmul_rn(lum, con), str);
+  if (!(score > 0.f)) return ~0ull;
+  return ((uint64_t)(0x7FFFFFFFu - __float_as_uint(score)) << 32) |
+         ((uint32_t)(dy + 32768) << 16) | (uint32_t)(dx + 32768);
 }
 
 }  // namespace
@@ -194,15 +218,18 @@ __global__ __launch_bounds__(256) void me_ssim_stats_kernel(SearchArgs p, SsimPl
   }
 }
 
-__global__ __launch_bounds__(SSIM_THREADS) void me_ssim_kernel(SearchArgs p, int row0,
+// Blocks [row0, ..) x [col0, nbx) of the launch's rows (grid = rows x (nbx - col0)).
+__global__ __launch_bounds__(SSIM_THREADS) void me_ssim_kernel(SearchArgs p, int row0, int col0,
                                                                int win_lds_bytes,
                                                                const float2* stats, SsimPlane pg) {
   extern __shared__ __align__(16) uint8_t smem[];
   __shared__ uint64_t red[SSIM_THREADS / 64];
   __shared__ float ccl[256];  // 16 x 16 blocks with the statistics plane: (c - imc) as floats
-  const int tid = threadIdx.x;
-  const int bx = (int)(blockIdx.x % (unsigned)p.nbx);
-  const int by = row0 + (int)(blockIdx.x / (unsigned)p.nbx);
+  __shared__ float cstat[2];  // the current block's mean and variance
+  const int tid = threadIdx.x, nt = (int)blockDim.x;
+  const int ncol = p.nbx - col0;
+  const int bx = col0 + (int)(blockIdx.x % (unsigned)ncol);
+  const int by = row0 + (int)(blockIdx.x / (unsigned)ncol);
   const int B = p.blk, S = p.range;
   const int tlx = bx * B, tly = by * B;
   const int w = min(B, p.width - tlx), h = min(B, p.height - tly);
@@ -214,23 +241,32 @@ __global__ __launch_bounds__(SSIM_THREADS) void me_ssim_kernel(SearchArgs p, int
   uint8_t* cblk = smem;                        // w*h bytes, pitch w
   uint8_t* win = smem + ((B * B + 15) & ~15);  // ww*wh bytes when staged
   const bool staged = win_lds_bytes >= ww * wh;
-  for (int i = tid; i < w * h; i += SSIM_THREADS) {
+  for (int i = tid; i < w * h; i += nt) {
     const int oy = i / w, ox = i - oy * w;
     cblk[i] = p.cur[(ptrdiff_t)(tly + oy - p.cur_row0) * p.stride + tlx + ox];
   }
   if (staged)
-    for (int i = tid; i < ww * wh; i += SSIM_THREADS) {
+    for (int i = tid; i < ww * wh; i += nt) {
       const int oy = i / ww, ox = i - oy * ww;
       win[i] = p.ref[(ptrdiff_t)(wy0 + oy - p.ref_row0) * p.stride + wx0 + ox];
     }
   __syncthreads();
 
   const float nf = (float)(w * h);
-  const float C1 = 0.01f, C2 = 0.09f, C3 = 0.045f;  // ssim.c:48
   // Statistics of the current block (the reference recomputes them for every
-  // candidate; they are the same numbers).
-  float mp, vp;
-  patch_stats(cblk, w, w, h, nf, &mp, &vp);
+  // candidate; they are the same numbers): one serial float chain, run by
+  // wave 0 alone (every wave running it cost ~1/6 of a 16 x 16 workgroup's
+  // VALU issue) and handed over in LDS.
+  if (tid < 64) {
+    float m0, v0;
+    patch_stats(cblk, w, w, h, nf, &m0, &v0);
+    if (tid == 0) {
+      cstat[0] = m0;
+      cstat[1] = v0;
+    }
+  }
+  __syncthreads();
+  const float mp = cstat[0], vp = cstat[1];
   const float sp = sqrt_via_double(vp);
   const int imp = (int)mp;  // truncation, as the int parameter of computeCrossVar
 
@@ -241,18 +277,15 @@ __global__ __launch_bounds__(SSIM_THREADS) void me_ssim_kernel(SearchArgs p, int
   const int ngx = (ncx + SSIM_Q - 1) / SSIM_Q;
   const int ngroups = ngx * ncy;
   // ssim.c:53-56 for candidate (cx0 + k, cy) of a group: the key, or ~0
+  // cv / nf: nf = w h a power of two (the full 16 x 16 and 8 x 8 blocks)
+  // divides exactly as a multiplication by 1 / nf (both are the correctly
+  // rounded x 2^-k); the 10-instruction division otherwise
+  const int nfi = w * h;
+  const bool pow2 = (nfi & (nfi - 1)) == 0;
+  const float inv_nf = 1.0f / nf;  // exact when nf is a power of two
   auto key_of = [&](float m, float sr, float cvsum, int cx, int cy) -> uint64_t {
-    const float cvk = __fdiv_rn(cvsum, nf);
-    const float lum = __fdiv_rn(__fadd_rn(__fmul_rn(__fmul_rn(2.f, m), mp), C1),
-                                __fadd_rn(__fadd_rn(__fmul_rn(m, m), __fmul_rn(mp, mp)), C1));
-    const float con = __fdiv_rn(__fadd_rn(__fmul_rn(__fmul_rn(2.f, sr), sp), C2),
-                                __fadd_rn(__fadd_rn(__fmul_rn(sr, sr), __fmul_rn(sp, sp)), C2));
-    const float str = __fdiv_rn(__fadd_rn(cvk, C3), __fadd_rn(__fmul_rn(sr, sp), C3));
-    const float score = __fmul_rn(__fmul_rn(lum, con), str);
-    if (!(score > 0.f)) return ~0ull;
-    const int dx = wx0 + cx - tlx, dy = wy0 + cy - tly;
-    return ((uint64_t)(0x7FFFFFFFu - __float_as_uint(score)) << 32) |
-           ((uint32_t)(dy + 32768) << 16) | (uint32_t)(dx + 32768);
+    const float cvk = pow2 ? __fmul_rn(cvsum, inv_nf) : __fdiv_rn(cvsum, nf);
+    return ssim_key(m, sr, cvk, mp, sp, wx0 + cx - tlx, wy0 + cy - tly);
   };
   if (stats != nullptr && B == 16 && w == 16 && h == 16 && staged) {
     // 16 x 16 blocks, window in LDS: per window row the lane's SSIM_Q16
@@ -260,10 +293,10 @@ __global__ __launch_bounds__(SSIM_THREADS) void me_ssim_kernel(SearchArgs p, int
     // block's (c - imc) as floats in LDS (broadcast reads), the row's 16 pixels
     // unrolled (no register shifts).  The same chains as below, in the same order.
     constexpr int Q = SSIM_Q16;
-    for (int i = tid; i < 256; i += SSIM_THREADS) ccl[i] = (float)(cblk[i] - imp);
+    for (int i = tid; i < 256; i += nt) ccl[i] = (float)(cblk[i] - imp);
     __syncthreads();
     const int ngq = (ncx + Q - 1) / Q, ng = ngq * ncy;
-    for (int t = tid; t < ng; t += SSIM_THREADS) {
+    for (int t = tid; t < ng; t += nt) {
       const int cy = t / ngq, cx0 = (t - cy * ngq) * Q;
       const uint8_t* r = win + cy * ww + cx0;  // past the window: the launch's SSIM_PAD bytes
       const float2* st = stats + (size_t)(wy0 + cy - pg.ylo) * pg.pitch;
@@ -300,7 +333,7 @@ __global__ __launch_bounds__(SSIM_THREADS) void me_ssim_kernel(SearchArgs p, int
     // exact in float) rounds once, exactly where the reference's add rounds.
     const int ngx8 = (ncx + SSIM_QP - 1) / SSIM_QP;
     const int ngroups8 = ngx8 * ncy;
-    for (int t = tid; t < ngroups8; t += SSIM_THREADS) {
+    for (int t = tid; t < ngroups8; t += nt) {
       const int cy = t / ngx8, cx0 = (t - cy * ngx8) * SSIM_QP;
       const uint8_t* r = staged ? win + cy * ww + cx0
                                 : p.ref + (ptrdiff_t)(wy0 + cy - p.ref_row0) * p.stride + wx0 + cx0;
@@ -338,7 +371,7 @@ __global__ __launch_bounds__(SSIM_THREADS) void me_ssim_kernel(SearchArgs p, int
       }
     }
   } else
-  for (int t = tid; t < ngroups; t += SSIM_THREADS) {
+  for (int t = tid; t < ngroups; t += nt) {
     const int cy = t / ngx, cx0 = (t - cy * ngx) * SSIM_Q;
     const uint8_t* r = staged ? win + cy * ww + cx0
                               : p.ref + (ptrdiff_t)(wy0 + cy - p.ref_row0) * p.stride + wx0 + cx0;
@@ -402,8 +435,177 @@ __global__ __launch_bounds__(SSIM_THREADS) void me_ssim_kernel(SearchArgs p, int
   __syncthreads();
   if (tid == 0) {
     uint64_t b = red[0];
+    for (int i = 1; i < nt / 64; i++) b = red[i] < b ? red[i] : b;
+    int dx = 0, dy = 0;
+    uint32_t bits = 0;
+    if (b != ~0ull) {
+      dx = (int)(b & 0xFFFF) - 32768;
+      dy = (int)((b >> 16) & 0xFFFF) - 32768;
+      bits = 0x7FFFFFFFu - (uint32_t)(b >> 32);
+    }
+    const int out = (by - p.block_row_begin) * p.nbx + bx;
+    p.mv[2 * out] = (int16_t)dx;
+    p.mv[2 * out + 1] = (int16_t)dy;
+    if (p.cost) p.cost[out] = bits;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// 16 x 16 blocks on the matrix cores.  The reference's cross variance is an
+// exact integer for a 16 x 16 block: each term (r - imr)(c - imc) is an int
+// with |term| <= 255^2, so every partial sum of the float chain
+// (computeCrossVar, ssim.c:30-42) is an integer below 256 * 255^2 =
+// 16,646,400 < 2^24 and exactly representable: the chain's result does not
+// depend on its order.  So
+//   cv = sum r c - imc S1r - imr S1c + 256 imr imc,
+//   sum r c = 127 S1r + 128 S1c - 4161536 - X,  X = sum (127 - c)(r - 128)
+// (S1r / S1c the patch / block byte sums, imr = S1r >> 8 = (int) mean_r, imc
+// likewise), and X is the i8 GEMM the SSD path already runs on
+// v_mfma_i32_16x16x64_i8 in the block-major layout (me_band.hip /
+// me_mfma.hip): one workgroup per block, 16 x 16 candidate tiles (16 x
+// positions by 16 y positions, 8 MFMAs each, K = two block rows in a 32-byte
+// span), and per candidate only the score's float operations in the
+// reference's order (ssim_key, as the float path) from the statistics plane's
+// mean and stddev.  The float path spent ~128 VALU per candidate on the chain.
+constexpr int SSIM_CREC = 48;                                // row record: 0^16, c ^ 0x7F, 0^16
+
+__host__ __device__ inline int ssim_mfma_lp(int S) { return 16 * ((2 * S + 15) / 16 + 3); }
+__host__ __device__ inline int ssim_mfma_rows(int S) { return 16 * ((2 * S + 1 + 15) / 16) + 15; }
+__host__ __device__ inline int ssim_mfma_lds(int S) {
+  return 256 + 16 * SSIM_CREC + ssim_mfma_rows(S) * ssim_mfma_lp(S);
+}
+
+__global__ __launch_bounds__(256) void me_ssim_mfma_kernel(SearchArgs p, int row0, int nbxf,
+                                                           const float2* stats, SsimPlane pg,
+                                                           int aligned16) {
+  extern __shared__ __align__(16) uint8_t smem[];
+  __shared__ uint64_t red[4];
+  __shared__ float cstat[2];
+  __shared__ int csum;
+  typedef int v4i __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(3))) const uint32_t lds_c32;
+  typedef __attribute__((address_space(3))) const v4i lds_cv4i;
+  auto lds_addr = [](const void* q) {
+    return (uint32_t)(uintptr_t)((__attribute__((address_space(3))) const uint8_t*)q);
+  };
+  const int tid = (int)threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n = lane & 15, hh = lane >> 4;
+  const int bx = (int)(blockIdx.x % (unsigned)nbxf), by = row0 + (int)(blockIdx.x / (unsigned)nbxf);
+  const int S = p.range, W = p.width, H = p.height;
+  const int tlx = 16 * bx, tly = 16 * by;
+  const int wx0 = max(tlx - S, 0), wy0 = max(tly - S, 0);
+  const int ncx = min(tlx + S, W - 16) - wx0 + 1, ncy = min(tly + S, H - 16) - wy0 + 1;
+  const int i0 = wx0 >> 4, ni = ((wx0 + ncx - 1) >> 4) - i0 + 1, nj = (ncy + 15) >> 4;
+  const int LP = ssim_mfma_lp(S), R = 16 * nj + 15;
+  uint8_t* cblk = smem;                        // the block, raw
+  uint8_t* crec = smem + 256;                  // 16 row records
+  uint8_t* win = crec + 16 * SSIM_CREC;        // rows wy0 .., columns 16 i0 ..: r ^ 0x80
+  for (int i = tid; i < 256; i += 256) {
+    const int oy = i >> 4, ox = i & 15;
+    const uint8_t c = p.cur[(ptrdiff_t)(tly + oy - p.cur_row0) * p.stride + tlx + ox];
+    cblk[i] = c;
+    crec[oy * SSIM_CREC + 16 + ox] = c ^ 0x7F;
+    crec[oy * SSIM_CREC + ox] = 0;
+    crec[oy * SSIM_CREC + 32 + ox] = 0;
+  }
+  // (columns and rows past the frame: zeros or the next bytes of the plane;
+  // only masked candidates read them)
+  if (aligned16) {
+    // 16-byte granules through a buffer resource over the resident rows
+    // (reads past it return 0)
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
+    const __amdgpu_buffer_rsrc_t rref =
+        __builtin_amdgcn_make_buffer_rsrc((void*)p.ref, (short)0, p.ref_bytes, 0x00020000);
+    const int G = LP >> 4;
+    for (int i = tid; i < R * G; i += 256) {
+      const int rr = i / G, gq = i - rr * G;
+      const uint32_t off = (uint32_t)((wy0 + rr - p.ref_row0) * p.stride + 16 * (i0 + gq));
+      const u32x4 v = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rref, off, 0, 0));
+      *reinterpret_cast<lds_u32x4*>((uintptr_t)(lds_addr(win) + 16u * (uint32_t)i)) = v ^ 0x80808080u;
+    }
+  } else {
+    for (int i = tid; i < R * LP; i += 256) {
+      const int rr = i / LP, col = i - rr * LP;
+      const int y = wy0 + rr, x = 16 * i0 + col;
+      win[i] = (y < H && x < W) ? (uint8_t)(p.ref[(ptrdiff_t)(y - p.ref_row0) * p.stride + x] ^ 0x80) : 0;
+    }
+  }
+  __syncthreads();
+  // the block's statistics (ssim.c:3-28 as the float path: one serial chain,
+  // wave 0) and byte sum
+  if (tid < 64) {
+    float m0, v0;
+    patch_stats(cblk, 16, 16, 16, 256.f, &m0, &v0);
+    int cs = 0;
+    for (int i = lane; i < 256; i += 64) cs += cblk[i];
 #pragma unroll
-    for (int i = 1; i < SSIM_THREADS / 64; i++) b = red[i] < b ? red[i] : b;
+    for (int off = 32; off > 0; off >>= 1) cs += __shfl_xor(cs, off, 64);
+    if (tid == 0) {
+      cstat[0] = m0;
+      cstat[1] = v0;
+      csum = cs;
+    }
+  }
+  // A fragments (me_band.hip's enter): lane (m = n, K group hh), fragment q =
+  // bytes o .. o + 15 of record row 2 q + (hh >> 1), o = 16 + 16 (hh & 1) - m
+  v4i A[8];
+  {
+    const int o = 16 + 16 * (hh & 1) - n, sh = o & 3;
+    const uint32_t lb = lds_addr(crec) + (uint32_t)((hh >> 1) * SSIM_CREC + (o & ~3));
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      uint32_t d[5];
+#pragma unroll
+      for (int e = 0; e < 5; e++)
+        d[e] = *reinterpret_cast<lds_c32*>((uintptr_t)(lb + (uint32_t)(2 * q * SSIM_CREC + 4 * e)));
+#pragma unroll
+      for (int e = 0; e < 4; e++) A[q][e] = (int)__builtin_amdgcn_alignbyte(d[e + 1], d[e], sh);
+    }
+  }
+  __syncthreads();
+  const float mp = cstat[0], sp = sqrt_via_double(cstat[1]);
+  const int S1c = csum, imc = S1c >> 8;  // (int) mp: S1c / 256, exact
+  const int kc = 128 * S1c - 4161536;
+  const float inv256 = 1.0f / 256.0f;
+  uint64_t best = ~0ull;
+  const uint32_t xb0 = lds_addr(win) + (uint32_t)((n + (hh >> 1)) * LP + 16 * (hh & 1));
+#pragma unroll 1
+  for (int t = wave; t < ni * nj; t += 4) {
+    const int tj = t / ni, ti = t - tj * ni;
+    // B fragment q: window row 16 tj + n + 2 q + (hh >> 1), column 16 ti + 16 (hh & 1)
+    const uint32_t xb = xb0 + (uint32_t)(16 * tj * LP + 16 * ti);
+    v4i f[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) f[q] = *reinterpret_cast<lds_cv4i*>((uintptr_t)(xb + (uint32_t)(2 * q * LP)));
+    v4i acc = {0, 0, 0, 0};
+#pragma unroll
+    for (int q = 0; q < 8; q++) acc = MFMA16(A[q], f[q], acc, 0, 0, 0);
+    // lane (n, hh): X of positions x = 16 (i0 + ti) + 4 hh + r, y = wy0 + 16 tj + n
+    const int cy = 16 * tj + n, cx0 = 16 * (i0 + ti) + 4 * hh - wx0;
+    if (cy < ncy) {
+      const float2* st = stats + (size_t)(wy0 + cy - pg.ylo) * pg.pitch + wx0;
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int cx = cx0 + r;
+        if (cx < 0 || cx >= ncx) continue;
+        const float2 v = st[cx];
+        const int S1r = (int)__fmul_rn(v.x, 256.f);  // mean_r = S1r / 256, exact
+        const int imr = S1r >> 8;
+        const int cv = 127 * S1r + kc - acc[r] - imc * S1r - imr * S1c + 256 * imr * imc;
+        const uint64_t key = ssim_key(v.x, v.y, __fmul_rn((float)cv, inv256), mp, sp,
+                                      wx0 + cx - tlx, wy0 + cy - tly);
+        best = key < best ? key : best;
+      }
+    }
+  }
+  best = wave_min(best);
+  if (lane == 0) red[wave] = best;
+  __syncthreads();
+  if (tid == 0) {
+    uint64_t b = red[0];
+#pragma unroll
+    for (int i = 1; i < 4; i++) b = red[i] < b ? red[i] : b;
     int dx = 0, dy = 0;
     uint32_t bits = 0;
     if (b != ~0ull) {
@@ -438,9 +640,38 @@ hipError_t launch_ssim(const SearchArgs& p, hipStream_t stream) {
                        dim3(256), 0, stream, p, sp, plane);
     stats = plane;
   }
+  // 16 x 16 blocks with the statistics plane, S <= 64: the full blocks (full
+  // height rows, full width columns) on the matrix cores, the partial right
+  // column and bottom row on the float path (second launch below)
+  int r_full = 0, nbxf = 0;
+  if (stats && B == 16 && p.range <= 64 && sp.pitch > 0) {
+    const int r0 = p.block_row_begin, r1 = p.block_row_end;
+    const int rfull_end = std::min(r1, p.height / 16);  // rows of full-height blocks
+    r_full = std::max(0, rfull_end - r0);
+    nbxf = p.width / 16;
+    if (r_full > 0 && nbxf > 0) {
+      const int a16 = p.stride % 16 == 0 && (uintptr_t)p.ref % 16 == 0 && p.ref_bytes > 0;
+      hipLaunchKernelGGL(me_ssim_mfma_kernel, dim3((unsigned)(r_full * nbxf)), dim3(256),
+                         ssim_mfma_lds(p.range), stream, p, r0, nbxf, stats, sp, a16);
+    } else {
+      r_full = 0;
+    }
+  }
   // + SSIM_PAD bytes: the last candidate group of the last row reads past the window
-  hipLaunchKernelGGL(me_ssim_kernel, dim3((unsigned)(rows * p.nbx)), dim3(SSIM_THREADS),
-                     cur + (int)win + SSIM_PAD, stream, p, p.block_row_begin, (int)win, stats, sp);
+  if (r_full == 0) {
+    hipLaunchKernelGGL(me_ssim_kernel, dim3((unsigned)(rows * p.nbx)), dim3(SSIM_THREADS),
+                       cur + (int)win + SSIM_PAD, stream, p, p.block_row_begin, 0, (int)win, stats, sp);
+  } else {
+    // the rest: the partial right column of the full rows, then any partial bottom row
+    if (nbxf < p.nbx)
+      hipLaunchKernelGGL(me_ssim_kernel, dim3((unsigned)(r_full * (p.nbx - nbxf))), dim3(SSIM_THREADS),
+                         cur + (int)win + SSIM_PAD, stream, p, p.block_row_begin, nbxf, (int)win, stats,
+                         sp);
+    if (p.block_row_begin + r_full < p.block_row_end)
+      hipLaunchKernelGGL(me_ssim_kernel, dim3((unsigned)((rows - r_full) * p.nbx)), dim3(SSIM_THREADS),
+                         cur + (int)win + SSIM_PAD, stream, p, p.block_row_begin + r_full, 0, (int)win,
+                         stats, sp);
+  }
   return hipGetLastError();
 }
 
