@@ -31,7 +31,10 @@
 // patches with the same float operations in the same order (ssim.c:3-28, the
 // same patch_stats as below), so they are the same bits; the search then runs
 // only the cross-term chain per candidate.  Blocks of a partial right column or
-// bottom row (w or h < B) keep the in-kernel statistics.
+// bottom row (w or h < B) keep the in-kernel statistics, except for 16 x 16
+// blocks (round 6): the full-width blocks of the partial bottom row get a
+// plane of 16 x (H % 16) patches and run on the matrix cores with the rest
+// (me_ssim_mfma_kernel below).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -124,10 +127,33 @@ static bool ssim_plane(const SearchArgs& p, SsimPlane* s) {
   return s->rows > 0;
 }
 
+// The partial bottom block row's plane (16 x 16 blocks, S <= 64, the row in
+// the search): entry (rr, x) = (mean, stddev) of the 16 x hbh ref patch at
+// row ylo + rr, column x, for every position its blocks can meet; the
+// matrix-core SSIM kernel runs that row too.
+static bool ssim_hb_plane(const SearchArgs& p, SsimPlane* s, int* hbh) {
+  const int S = p.range, W = p.width, H = p.height;
+  if (p.blk != 16 || S > 64 || W < 16 || H < 16 || H % 16 == 0) return false;
+  const int hb_row = H / 16;
+  if (hb_row < p.block_row_begin || hb_row >= p.block_row_end) return false;
+  *hbh = H - 16 * hb_row;
+  s->ylo = max(16 * hb_row - S, 0);
+  s->rows = H - *hbh - s->ylo + 1;
+  s->pitch = W - 15;
+  return s->rows > 0;
+}
+
+static size_t ssim_plane_bytes(const SsimPlane& s) {
+  return ((size_t)s.rows * (size_t)s.pitch * sizeof(float2) + 255) & ~(size_t)255;
+}
+
 size_t ssim_scratch(const SearchArgs& p) {
-  SsimPlane s;
-  if (p.cost_kind != COST_SSIM || !ssim_plane(p, &s)) return 0;
-  return (size_t)s.rows * (size_t)s.pitch * sizeof(float2);
+  if (p.cost_kind != COST_SSIM) return 0;
+  SsimPlane s, h;
+  int hbh;
+  size_t n = ssim_plane(p, &s) ? ssim_plane_bytes(s) : 0;
+  if (ssim_hb_plane(p, &h, &hbh)) n += ssim_plane_bytes(h);
+  return n;
 }
 
 // Workgroup = 64 columns x 16 rows of positions: the 16 + B - 1 ref rows they
@@ -185,20 +211,51 @@ __device__ __forceinline__ void stats_at(const uint32_t* t, int pr, int c, int B
   *v = __fdiv_rn(acc, nf);
 }
 
+// patch_stats of a 16-wide, hgt-row patch (the partial bottom row's, hgt < 16):
+// stats_at's operations with a runtime row count.
+__device__ __forceinline__ void stats_w16(const uint32_t* t, int pr, int c, int hgt, float* m,
+                                          float* v) {
+  const int a = c & 3, wb = c >> 2;
+  const float nf = (float)(16 * hgt);
+  auto word = [&](int i, int q) -> uint32_t {
+    const uint32_t* row = t + (pr + i) * STATS_TW + wb + q;
+    return __builtin_amdgcn_alignbyte(row[1], row[0], (uint32_t)a);
+  };
+  uint32_t s = 0;
+  for (int i = 0; i < hgt; i++)
+#pragma unroll
+    for (int q = 0; q < 4; q++) s = __builtin_amdgcn_sad_u8(word(i, q), 0u, s);
+  const float mf = __fdiv_rn((float)s, nf);
+  float acc = 0.f;
+  for (int i = 0; i < hgt; i++)
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const uint32_t w = word(i, q);
+#pragma unroll
+      for (int b = 0; b < 4; b++) {
+        const float d = __fsub_rn((float)((w >> (8 * b)) & 255u), mf);
+        acc = __fadd_rn(acc, __fmul_rn(d, d));
+      }
+    }
+  *m = mf;
+  *v = __fdiv_rn(acc, nf);
+}
+
+// ph: the patches' height (p.blk; the partial bottom row's plane: hbh < 16)
 __global__ __launch_bounds__(256) void me_ssim_stats_kernel(SearchArgs p, SsimPlane s,
-                                                            float2* plane) {
+                                                            float2* plane, int ph) {
   __shared__ uint32_t t[STATS_TR * STATS_TW];
   const int B = p.blk;
   const int x0 = (int)blockIdx.x * 64, y0 = (int)blockIdx.y * 16;
   const int tid = (int)threadIdx.x;
   uint8_t* tb = reinterpret_cast<uint8_t*>(t);
-  const int rows = 16 + B - 1;
+  const int rows = 16 + ph - 1;
   // row r, byte col <- ref(ylo + y0 + r, x0 + col); 0 past the frame or the
   // resident rows (never read by a position inside the plane)
   for (int i = tid; i < rows * STATS_TW * 4; i += 256) {
     const int r = i / (STATS_TW * 4), col = i - r * (STATS_TW * 4);
     const int y = s.ylo + y0 + r, xx = x0 + col;
-    tb[i] = (xx < p.width && y < s.ylo + s.rows + B - 1)
+    tb[i] = (xx < p.width && y < s.ylo + s.rows + ph - 1)
                 ? p.ref[(ptrdiff_t)(y - p.ref_row0) * p.stride + xx] : 0;
   }
   __syncthreads();
@@ -209,11 +266,14 @@ __global__ __launch_bounds__(256) void me_ssim_stats_kernel(SearchArgs p, SsimPl
     const int pr = 4 * g + j, rr = y0 + pr;
     if (rr >= s.rows) break;
     float m, v;
-    switch (B) {
-      case 16: stats_at<16>(t, pr, c, B, &m, &v); break;
-      case 8: stats_at<8>(t, pr, c, B, &m, &v); break;
-      default: stats_at<0>(t, pr, c, B, &m, &v); break;
-    }
+    if (ph != B)
+      stats_w16(t, pr, c, ph, &m, &v);
+    else
+      switch (B) {
+        case 16: stats_at<16>(t, pr, c, B, &m, &v); break;
+        case 8: stats_at<8>(t, pr, c, B, &m, &v); break;
+        default: stats_at<0>(t, pr, c, B, &m, &v); break;
+      }
     plane[(size_t)rr * s.pitch + x] = make_float2(m, sqrt_via_double(v));
   }
 }
@@ -475,9 +535,12 @@ __host__ __device__ inline int ssim_mfma_lds(int S) {
   return 256 + 16 * SSIM_CREC + ssim_mfma_rows(S) * ssim_mfma_lp(S);
 }
 
+// bh: the blocks' height -- 16, or the partial bottom row's H % 16 (its own
+// statistics plane; N = 16 bh pixels <= 256, so the identity above holds with
+// 256 -> N and 4161536 -> 16256 N; record rows >= bh are zero)
 __global__ __launch_bounds__(256) void me_ssim_mfma_kernel(SearchArgs p, int row0, int nbxf,
                                                            const float2* stats, SsimPlane pg,
-                                                           int aligned16) {
+                                                           int aligned16, int bh) {
   extern __shared__ __align__(16) uint8_t smem[];
   __shared__ uint64_t red[4];
   __shared__ float cstat[2];
@@ -494,7 +557,7 @@ __global__ __launch_bounds__(256) void me_ssim_mfma_kernel(SearchArgs p, int row
   const int S = p.range, W = p.width, H = p.height;
   const int tlx = 16 * bx, tly = 16 * by;
   const int wx0 = max(tlx - S, 0), wy0 = max(tly - S, 0);
-  const int ncx = min(tlx + S, W - 16) - wx0 + 1, ncy = min(tly + S, H - 16) - wy0 + 1;
+  const int ncx = min(tlx + S, W - 16) - wx0 + 1, ncy = min(tly + S, H - bh) - wy0 + 1;
   const int i0 = wx0 >> 4, ni = ((wx0 + ncx - 1) >> 4) - i0 + 1, nj = (ncy + 15) >> 4;
   const int LP = ssim_mfma_lp(S), R = 16 * nj + 15;
   uint8_t* cblk = smem;                        // the block, raw
@@ -502,9 +565,9 @@ __global__ __launch_bounds__(256) void me_ssim_mfma_kernel(SearchArgs p, int row
   uint8_t* win = crec + 16 * SSIM_CREC;        // rows wy0 .., columns 16 i0 ..: r ^ 0x80
   for (int i = tid; i < 256; i += 256) {
     const int oy = i >> 4, ox = i & 15;
-    const uint8_t c = p.cur[(ptrdiff_t)(tly + oy - p.cur_row0) * p.stride + tlx + ox];
+    const uint8_t c = oy < bh ? p.cur[(ptrdiff_t)(tly + oy - p.cur_row0) * p.stride + tlx + ox] : 0;
     cblk[i] = c;
-    crec[oy * SSIM_CREC + 16 + ox] = c ^ 0x7F;
+    crec[oy * SSIM_CREC + 16 + ox] = oy < bh ? c ^ 0x7F : 0;
     crec[oy * SSIM_CREC + ox] = 0;
     crec[oy * SSIM_CREC + 32 + ox] = 0;
   }
@@ -534,11 +597,12 @@ __global__ __launch_bounds__(256) void me_ssim_mfma_kernel(SearchArgs p, int row
   __syncthreads();
   // the block's statistics (ssim.c:3-28 as the float path: one serial chain,
   // wave 0) and byte sum
+  const int N = 16 * bh;
   if (tid < 64) {
     float m0, v0;
-    patch_stats(cblk, 16, 16, 16, 256.f, &m0, &v0);
+    patch_stats(cblk, 16, 16, bh, (float)N, &m0, &v0);
     int cs = 0;
-    for (int i = lane; i < 256; i += 64) cs += cblk[i];
+    for (int i = lane; i < 256; i += 64) cs += cblk[i];  // rows >= bh: 0
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) cs += __shfl_xor(cs, off, 64);
     if (tid == 0) {
@@ -565,9 +629,12 @@ __global__ __launch_bounds__(256) void me_ssim_mfma_kernel(SearchArgs p, int row
   }
   __syncthreads();
   const float mp = cstat[0], sp = sqrt_via_double(cstat[1]);
-  const int S1c = csum, imc = S1c >> 8;  // (int) mp: S1c / 256, exact
-  const int kc = 128 * S1c - 4161536;
-  const float inv256 = 1.0f / 256.0f;
+  // (int) mp = S1c / N: the rounded quotient stays below the next integer
+  // (1 - frac >= 1 / N is far above its ulp)
+  const int S1c = csum, imc = (int)mp;
+  const int kc = 128 * S1c - 16256 * N;
+  const float nf = (float)N, inv_nf = 1.0f / nf;  // exact when N is a power of two
+  const bool pow2 = (N & (N - 1)) == 0;
   uint64_t best = ~0ull;
   const uint32_t xb0 = lds_addr(win) + (uint32_t)((n + (hh >> 1)) * LP + 16 * (hh & 1));
 #pragma unroll 1
@@ -590,11 +657,12 @@ __global__ __launch_bounds__(256) void me_ssim_mfma_kernel(SearchArgs p, int row
         const int cx = cx0 + r;
         if (cx < 0 || cx >= ncx) continue;
         const float2 v = st[cx];
-        const int S1r = (int)__fmul_rn(v.x, 256.f);  // mean_r = S1r / 256, exact
-        const int imr = S1r >> 8;
-        const int cv = 127 * S1r + kc - acc[r] - imc * S1r - imr * S1c + 256 * imr * imc;
-        const uint64_t key = ssim_key(v.x, v.y, __fmul_rn((float)cv, inv256), mp, sp,
-                                      wx0 + cx - tlx, wy0 + cy - tly);
+        // mean_r = fl(S1r / N): N mean_r is within N ulp / 2 < 1/2 of S1r
+        const int S1r = __float2int_rn(__fmul_rn(v.x, nf));
+        const int imr = (int)v.x;
+        const int cv = 127 * S1r + kc - acc[r] - imc * S1r - imr * S1c + N * imr * imc;
+        const float cvk = pow2 ? __fmul_rn((float)cv, inv_nf) : __fdiv_rn((float)cv, nf);
+        const uint64_t key = ssim_key(v.x, v.y, cvk, mp, sp, wx0 + cx - tlx, wy0 + cy - tly);
         best = key < best ? key : best;
       }
     }
@@ -628,49 +696,67 @@ hipError_t launch_ssim(const SearchArgs& p, hipStream_t stream) {
   long win = (long)(B + 2 * p.range) * (B + 2 * p.range);
   const int cur = (B * B + 15) & ~15;
   if (cur + win + SSIM_PAD > GENERIC_LDS_BUDGET) win = 0;  // read the window from global memory
-  // Patch statistics plane in the context scratch when it holds one (attach_scratch
-  // sizes it with ssim_scratch); otherwise every block computes its own.
-  SsimPlane sp{0, 0, 0};
+  // Patch statistics planes in the context scratch when it holds them
+  // (attach_scratch sizes it with ssim_scratch); otherwise every block computes
+  // its own.  The full rows' plane first, then the partial bottom row's.
+  SsimPlane sp{0, 0, 0}, hp{0, 0, 0};
   const float2* stats = nullptr;
+  const float2* hstats = nullptr;
+  int hbh = 0;
   const size_t need = ssim_scratch(p);
-  if (need && p.scratch && p.scratch_bytes >= need && ssim_plane(p, &sp)) {
-    float2* plane = reinterpret_cast<float2*>(p.scratch);
-    hipLaunchKernelGGL(me_ssim_stats_kernel, dim3((unsigned)((sp.pitch + 63) / 64),
-                                                  (unsigned)((sp.rows + 15) / 16)),
-                       dim3(256), 0, stream, p, sp, plane);
-    stats = plane;
-  }
-  // 16 x 16 blocks with the statistics plane, S <= 64: the full blocks (full
-  // height rows, full width columns) on the matrix cores, the partial right
-  // column and bottom row on the float path (second launch below)
-  int r_full = 0, nbxf = 0;
-  if (stats && B == 16 && p.range <= 64 && sp.pitch > 0) {
-    const int r0 = p.block_row_begin, r1 = p.block_row_end;
-    const int rfull_end = std::min(r1, p.height / 16);  // rows of full-height blocks
-    r_full = std::max(0, rfull_end - r0);
-    nbxf = p.width / 16;
-    if (r_full > 0 && nbxf > 0) {
-      const int a16 = p.stride % 16 == 0 && (uintptr_t)p.ref % 16 == 0 && p.ref_bytes > 0;
-      hipLaunchKernelGGL(me_ssim_mfma_kernel, dim3((unsigned)(r_full * nbxf)), dim3(256),
-                         ssim_mfma_lds(p.range), stream, p, r0, nbxf, stats, sp, a16);
-    } else {
-      r_full = 0;
+  if (need && p.scratch && p.scratch_bytes >= need) {
+    uint8_t* base = reinterpret_cast<uint8_t*>(p.scratch);
+    if (ssim_plane(p, &sp)) {
+      float2* plane = reinterpret_cast<float2*>(base);
+      hipLaunchKernelGGL(me_ssim_stats_kernel, dim3((unsigned)((sp.pitch + 63) / 64),
+                                                    (unsigned)((sp.rows + 15) / 16)),
+                         dim3(256), 0, stream, p, sp, plane, B);
+      stats = plane;
+      base += ssim_plane_bytes(sp);
+    }
+    if (ssim_hb_plane(p, &hp, &hbh)) {
+      float2* plane = reinterpret_cast<float2*>(base);
+      hipLaunchKernelGGL(me_ssim_stats_kernel, dim3((unsigned)((hp.pitch + 63) / 64),
+                                                    (unsigned)((hp.rows + 15) / 16)),
+                         dim3(256), 0, stream, p, hp, plane, hbh);
+      hstats = plane;
     }
   }
+  // 16 x 16 blocks with the statistics planes, S <= 64: the full-width columns
+  // on the matrix cores (full rows, then the partial bottom row with its own
+  // plane); the partial right column on the float path
+  const int a16 = p.stride % 16 == 0 && (uintptr_t)p.ref % 16 == 0 && p.ref_bytes > 0;
+  const int nbxf = B == 16 && p.range <= 64 ? p.width / 16 : 0;
+  int r_full = 0;
+  if (stats && nbxf > 0) {
+    r_full = std::max(0, std::min(p.block_row_end, p.height / 16) - p.block_row_begin);
+    if (r_full > 0)
+      hipLaunchKernelGGL(me_ssim_mfma_kernel, dim3((unsigned)(r_full * nbxf)), dim3(256),
+                         ssim_mfma_lds(p.range), stream, p, p.block_row_begin, nbxf, stats, sp, a16,
+                         16);
+  }
+  const bool hb_mfma = hstats && nbxf > 0;
+  if (hb_mfma)
+    hipLaunchKernelGGL(me_ssim_mfma_kernel, dim3((unsigned)nbxf), dim3(256), ssim_mfma_lds(p.range),
+                       stream, p, p.height / 16, nbxf, hstats, hp, a16, hbh);
   // + SSIM_PAD bytes: the last candidate group of the last row reads past the window
-  if (r_full == 0) {
-    hipLaunchKernelGGL(me_ssim_kernel, dim3((unsigned)(rows * p.nbx)), dim3(SSIM_THREADS),
-                       cur + (int)win + SSIM_PAD, stream, p, p.block_row_begin, 0, (int)win, stats, sp);
+  const int lds = cur + (int)win + SSIM_PAD;
+  if (r_full == 0 && !hb_mfma) {
+    hipLaunchKernelGGL(me_ssim_kernel, dim3((unsigned)(rows * p.nbx)), dim3(SSIM_THREADS), lds, stream,
+                       p, p.block_row_begin, 0, (int)win, stats, sp);
   } else {
-    // the rest: the partial right column of the full rows, then any partial bottom row
-    if (nbxf < p.nbx)
+    // the rest: the partial right column of the full rows, then the partial
+    // bottom row (its right-column block only when the row ran on the matrix cores)
+    if (r_full > 0 && nbxf < p.nbx)
       hipLaunchKernelGGL(me_ssim_kernel, dim3((unsigned)(r_full * (p.nbx - nbxf))), dim3(SSIM_THREADS),
-                         cur + (int)win + SSIM_PAD, stream, p, p.block_row_begin, nbxf, (int)win, stats,
-                         sp);
-    if (p.block_row_begin + r_full < p.block_row_end)
-      hipLaunchKernelGGL(me_ssim_kernel, dim3((unsigned)((rows - r_full) * p.nbx)), dim3(SSIM_THREADS),
-                         cur + (int)win + SSIM_PAD, stream, p, p.block_row_begin + r_full, 0, (int)win,
-                         stats, sp);
+                         lds, stream, p, p.block_row_begin, nbxf, (int)win, stats, sp);
+    const int rb = p.block_row_begin + r_full;
+    if (rb < p.block_row_end) {
+      const int col0 = hb_mfma ? nbxf : 0;
+      if (col0 < p.nbx)
+        hipLaunchKernelGGL(me_ssim_kernel, dim3((unsigned)((p.block_row_end - rb) * (p.nbx - col0))),
+                           dim3(SSIM_THREADS), lds, stream, p, rb, col0, (int)win, stats, sp);
+    }
   }
   return hipGetLastError();
 }

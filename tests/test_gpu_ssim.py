@@ -89,3 +89,42 @@ def test_ssim_reference_interface(engine, manifest):
     s = me.find_best_blk_ssim(pf, f1, blk, 7, engine=engine)
     assert np.float32(s).view(np.uint32) == gscore.view(np.uint32)[57]
     assert [blk.motion_vectorX, blk.motion_vectorY] == gmv[57].tolist()
+
+
+@pytest.mark.parametrize("span", [0, 3, 16, 33, 64])
+def test_ssim_partial_bottom_row_every_height(engine, span):
+    """16 x 16 blocks: the full-width blocks of a partial bottom row (H % 16 =
+    1 .. 15; N = 16 (H % 16) pixels, powers of two and not) run on the matrix
+    cores from their own 16 x (H % 16) statistics plane; smooth, flat and
+    binary frames, a partial right column beside them."""
+    rng = np.random.default_rng(600 + span)
+    for hbh in range(1, 16):
+        h, w = 16 * 3 + hbh, 16 * 5 + (hbh % 3) * 5
+        kind = ("smooth", "flat", "binary")[hbh % 3]
+        if kind == "smooth":
+            ref, cur = synth.frame_pair(w, h, hbh + span, 2, -1)
+        elif kind == "flat":
+            ref = np.full((h, w), 97, np.uint8)
+            ref[::3] = 98
+            cur = np.full((h, w), 97, np.uint8)
+            cur[:, ::5] = 40
+        else:
+            ref = (rng.integers(0, 2, (h, w)) * 255).astype(np.uint8)
+            cur = (rng.integers(0, 2, (h, w)) * 255).astype(np.uint8)
+        mv, bits = engine.full_search(ref, cur, 16, span, "ssim")
+        omv, obits, _ = O.full_search(ref, cur, 16, span, "ssim")
+        what = f"{w}x{h} S{span} {kind}"
+        np.testing.assert_array_equal(bits, obits, err_msg=what)
+        np.testing.assert_array_equal(mv, omv, err_msg=what)
+
+
+def test_ssim_partial_bottom_row_alone_on_a_device():
+    """A device list that leaves one device only the partial bottom row (and
+    one a run of full rows ending at it): each launch builds the planes it needs."""
+    ref, cur = synth.frame_pair(200, 16 * 4 + 12, 31, 3, 2)
+    omv, obits, _ = O.full_search(ref, cur, 16, 20, "ssim")
+    for devs in ([0, 0, 0, 0, 0], [0, 0]):
+        with me.Engine(devices=devs) as eng:
+            mv, bits = eng.full_search(ref, cur, 16, 20, "ssim")
+        np.testing.assert_array_equal(bits, obits, err_msg=str(devs))
+        np.testing.assert_array_equal(mv, omv, err_msg=str(devs))
