@@ -105,14 +105,52 @@ __device__ __forceinline__ uint64_t ssim_key(float m, float sr, float cvk, float
          ((uint32_t)(dy + 32768) << 16) | (uint32_t)(dx + 32768);
 }
 
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+// a / b for two lane-halves, correctly rounded: the compiler's f32 division
+// (v_div_scale, v_rcp_f32, the Newton / residual fma chain, v_div_fmas,
+// v_div_fixup) without the scaling and fix-up steps.  Those are the identity
+// when |a| and |b| lie in [2^-40, 2^40]: v_div_scale scales only for an
+// exponent gap >= 96, a denormal or near-denormal numerator, or a denominator
+// whose reciprocal is denormal, and v_div_fixup changes only NaN / inf / zero /
+// overflowed results.  So these are __fdiv_rn's bits, two quotients per packed
+// fma, for the SSIM score's operands, which stay in that range whatever the
+// frame (means in [0, 255], stddevs in [0, 127.5], C1..C3 > 0.009):
+//   lum  (2m mp + C1) / (m^2 + mp^2 + C1)       both in [0.01, 130051]
+//   con  (2sr sp + C2) / (sr^2 + sp^2 + C2)     both in [0.09, 32514]
+//   str  (cv / N + C3) / (sr sp + C3)           |cv / N + C3| in [2^-17, 2^27]
+// (cv an integer: cv / N + 0.045 is never 0 for N = 16 k <= 256 and stays
+// above 2^-17 in magnitude; |cv| < 2^31).  tests/test_gpu_ssim.py and the
+// reference's goldens pin the bits.
+__device__ __forceinline__ f2v div_rn2(f2v a, f2v b) {
+  const f2v one = {1.f, 1.f};
+  f2v y = {__builtin_amdgcn_rcpf(b.x), __builtin_amdgcn_rcpf(b.y)};
+  const f2v e = __builtin_elementwise_fma(-b, y, one);
+  y = __builtin_elementwise_fma(e, y, y);
+  f2v q = a * y;
+  f2v r = __builtin_elementwise_fma(-b, q, a);
+  q = __builtin_elementwise_fma(r, y, q);
+  r = __builtin_elementwise_fma(-b, q, a);
+  return __builtin_elementwise_fma(r, y, q);
+}
+
 }  // namespace
 
 // Statistics plane: entry (rr, x) = (mean, stddev) of the B x B ref patch at
 // frame row ylo + rr, column x (x in [0, W - B]), for every position a full
 // block of block rows [block_row_begin, block_row_end) can meet.
+// 16 x 16 blocks with S <= 64 (the matrix-core kernel reads the plane) store
+// it compact: stddev as float [rows][ld], then the patch byte sum S1r as u16
+// [rows][ld] (the mean is S1r / N, exact for N = 256, and fl(S1r / N)
+// otherwise), ld a multiple of 64 entries: a lane's four adjacent candidates
+// are one 16-byte and one 8-byte load (float2 entries took four 8-byte loads,
+// 32 tag lookups per wave each: ~49 of the kernel's 115 us at 1080p,
+// profiles/r06q_*).  Other shapes: float2 (mean, stddev) [rows][ld = pitch].
 struct SsimPlane {
-  int ylo, rows, pitch;
+  int ylo, rows, pitch, ld, compact;
 };
+
+static bool ssim_compact(const SearchArgs& p) { return p.blk == 16 && p.range <= 64; }
 
 static bool ssim_plane(const SearchArgs& p, SsimPlane* s) {
   const int B = p.blk, S = p.range, W = p.width, H = p.height;
@@ -124,6 +162,8 @@ static bool ssim_plane(const SearchArgs& p, SsimPlane* s) {
   s->ylo = max(r0 * B - S, 0);
   s->rows = min((r1 - 1) * B + S, H - B) - s->ylo + 1;
   s->pitch = W - B + 1;
+  s->compact = ssim_compact(p);
+  s->ld = s->compact ? (s->pitch + 15 + 63) & ~63 : s->pitch;  // >= W: a tile's last column
   return s->rows > 0;
 }
 
@@ -140,11 +180,20 @@ static bool ssim_hb_plane(const SearchArgs& p, SsimPlane* s, int* hbh) {
   s->ylo = max(16 * hb_row - S, 0);
   s->rows = H - *hbh - s->ylo + 1;
   s->pitch = W - 15;
+  s->compact = 1;
+  s->ld = (s->pitch + 15 + 63) & ~63;
   return s->rows > 0;
 }
 
 static size_t ssim_plane_bytes(const SsimPlane& s) {
-  return ((size_t)s.rows * (size_t)s.pitch * sizeof(float2) + 255) & ~(size_t)255;
+  return ((size_t)s.rows * (size_t)s.ld * (s.compact ? 6 : sizeof(float2)) + 255) & ~(size_t)255;
+}
+
+// 16 x 16 blocks on the matrix cores: (mean, stddev, byte sum) of each
+// full-width current block of the launch's rows
+static size_t ssim_cur_stats_bytes(const SearchArgs& p) {
+  if (p.blk != 16 || p.range > 64 || p.width < 16) return 0;
+  return (size_t)(p.block_row_end - p.block_row_begin) * (size_t)(p.width / 16) * sizeof(float4);
 }
 
 size_t ssim_scratch(const SearchArgs& p) {
@@ -153,7 +202,7 @@ size_t ssim_scratch(const SearchArgs& p) {
   int hbh;
   size_t n = ssim_plane(p, &s) ? ssim_plane_bytes(s) : 0;
   if (ssim_hb_plane(p, &h, &hbh)) n += ssim_plane_bytes(h);
-  return n;
+  return n ? n + ssim_cur_stats_bytes(p) : 0;
 }
 
 // Workgroup = 64 columns x 16 rows of positions: the 16 + B - 1 ref rows they
@@ -241,13 +290,119 @@ __device__ __forceinline__ void stats_w16(const uint32_t* t, int pr, int c, int 
   *v = __fdiv_rn(acc, nf);
 }
 
-// ph: the patches' height (p.blk; the partial bottom row's plane: hbh < 16)
-__global__ __launch_bounds__(256) void me_ssim_stats_kernel(SearchArgs p, SsimPlane s,
-                                                            float2* plane, int ph) {
+// stats_at<16> for the positions at rows pr and pr + 1 of column c at once:
+// the same operations per position, in the same order, two positions per
+// packed fp32 instruction (v_pk_add_f32 / v_pk_mul_f32, each lane-half
+// rounded as the scalar instruction), the 17 staged rows' words aligned once.
+__device__ __forceinline__ void stats16_pair(const uint32_t* t, int pr, int c, float2* m,
+                                             float2* v) {
+  typedef float f2v __attribute__((ext_vector_type(2)));
+  const int a = c & 3, wb = c >> 2;
+  uint32_t w[17][4];
+#pragma unroll
+  for (int i = 0; i < 17; i++) {
+    const uint32_t* row = t + (pr + i) * STATS_TW + wb;
+    uint32_t d[5];
+#pragma unroll
+    for (int e = 0; e < 5; e++) d[e] = row[e];
+#pragma unroll
+    for (int q = 0; q < 4; q++) w[i][q] = __builtin_amdgcn_alignbyte(d[q + 1], d[q], (uint32_t)a);
+  }
+  uint32_t sa = 0, sb = 0;
+#pragma unroll
+  for (int i = 0; i < 16; i++)
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      sa = __builtin_amdgcn_sad_u8(w[i][q], 0u, sa);
+      sb = __builtin_amdgcn_sad_u8(w[i + 1][q], 0u, sb);
+    }
+  // sums / 256: exact, as __fdiv_rn(s, 256.f)
+  const f2v mf = {__fmul_rn((float)sa, 1.0f / 256.0f), __fmul_rn((float)sb, 1.0f / 256.0f)};
+  f2v acc = {0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < 16; i++)
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+#pragma unroll
+      for (int b = 0; b < 4; b++) {
+        const f2v x = {(float)((w[i][q] >> (8 * b)) & 255u), (float)((w[i + 1][q] >> (8 * b)) & 255u)};
+        const f2v d = x - mf;
+        acc = acc + d * d;
+      }
+  *m = make_float2(mf.x, mf.y);
+  *v = make_float2(__fmul_rn(acc.x, 1.0f / 256.0f), __fmul_rn(acc.y, 1.0f / 256.0f));
+}
+
+// One launch for every statistic the search reads: grid rows [0, gy[0]) the
+// current blocks' (mean, stddev, byte sum) for the matrix-core kernel, then
+// gy[1] rows of tiles of plane 1 (the full rows'), gy[2] of plane 2 (the
+// partial bottom row's, patch height ph[2] < 16).
+struct SsimStatsJob {
+  SsimPlane pl[3];
+  float2* out[3];
+  int ph[3], gy[3];
+  float4* cst;      // current blocks: (by - block_row_begin) nbxf + bx
+  int cst_n, nbxf;  // entries, full-width columns
+  int cur_a4;       // current rows 4-byte aligned
+};
+
+// The current block at (bx, by) from global memory: ssim.c:3-28 in the float
+// path's order (patch_stats), and the integer byte sum.
+__device__ __forceinline__ float4 cur_block_stats(const SearchArgs& p, int bx, int by, int a4) {
+  const int bh = min(16, p.height - 16 * by);
+  const uint8_t* src = p.cur + (ptrdiff_t)(16 * by - p.cur_row0) * p.stride + 16 * bx;
+  uint32_t w[16][4];
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    const uint8_t* row = src + (ptrdiff_t)min(i, bh - 1) * p.stride;
+    if (a4) {
+#pragma unroll
+      for (int q = 0; q < 4; q++) w[i][q] = reinterpret_cast<const uint32_t*>(row)[q];
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+        w[i][q] = (uint32_t)row[4 * q] | (uint32_t)row[4 * q + 1] << 8 |
+                  (uint32_t)row[4 * q + 2] << 16 | (uint32_t)row[4 * q + 3] << 24;
+    }
+  }
+  uint32_t s = 0;
+#pragma unroll
+  for (int i = 0; i < 16; i++)
+    if (i < bh)
+#pragma unroll
+      for (int q = 0; q < 4; q++) s = __builtin_amdgcn_sad_u8(w[i][q], 0u, s);
+  const float nf = (float)(16 * bh);
+  const float m = __fdiv_rn((float)s, nf);
+  float acc = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; i++)
+    if (i < bh)
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+          const float d = __fsub_rn((float)((w[i][q] >> (8 * b)) & 255u), m);
+          acc = __fadd_rn(acc, __fmul_rn(d, d));
+        }
+  return make_float4(m, sqrt_via_double(__fdiv_rn(acc, nf)), __int_as_float((int)s), 0.f);
+}
+
+__global__ __launch_bounds__(256) void me_ssim_stats_kernel(SearchArgs p, SsimStatsJob J) {
   __shared__ uint32_t t[STATS_TR * STATS_TW];
   const int B = p.blk;
-  const int x0 = (int)blockIdx.x * 64, y0 = (int)blockIdx.y * 16;
   const int tid = (int)threadIdx.x;
+  int yb = (int)blockIdx.y, k = 0;
+  while (k < 2 && yb >= J.gy[k]) yb -= J.gy[k++];
+  if (k == 0) {
+    const int e = (yb * (int)gridDim.x + (int)blockIdx.x) * 256 + tid;
+    if (e < J.cst_n)
+      J.cst[e] = cur_block_stats(p, e % J.nbxf, p.block_row_begin + e / J.nbxf, J.cur_a4);
+    return;
+  }
+  const SsimPlane s = J.pl[k];
+  float2* const plane = J.out[k];
+  const int ph = J.ph[k];
+  const int x0 = (int)blockIdx.x * 64, y0 = yb * 16;
   uint8_t* tb = reinterpret_cast<uint8_t*>(t);
   const int rows = 16 + ph - 1;
   // row r, byte col <- ref(ylo + y0 + r, x0 + col); 0 past the frame or the
@@ -261,6 +416,30 @@ __global__ __launch_bounds__(256) void me_ssim_stats_kernel(SearchArgs p, SsimPl
   __syncthreads();
   const int c = tid & 63, g = tid >> 6, x = x0 + c;
   if (x >= s.pitch) return;
+  const float nfp = (float)(B * ph);
+  auto put = [&](int rr, float m, float v) {
+    const size_t e = (size_t)rr * s.ld + x;
+    if (s.compact) {
+      float* sd = reinterpret_cast<float*>(plane);
+      sd[e] = sqrt_via_double(v);
+      // m = fl(S1r / N): N m is within N ulp / 2 < 1/2 of the integer S1r
+      reinterpret_cast<uint16_t*>(sd + (size_t)s.rows * s.ld)[e] = (uint16_t)__float2int_rn(__fmul_rn(m, nfp));
+    } else {
+      plane[e] = make_float2(m, sqrt_via_double(v));
+    }
+  };
+  if (B == 16 && ph == 16) {
+#pragma unroll 1
+    for (int j = 0; j < 4; j += 2) {
+      const int pr = 4 * g + j, rr = y0 + pr;
+      if (rr >= s.rows) break;
+      float2 m, v;
+      stats16_pair(t, pr, c, &m, &v);  // row pr + 1 + 15 <= 30: staged
+      put(rr, m.x, v.x);
+      if (rr + 1 < s.rows) put(rr + 1, m.y, v.y);
+    }
+    return;
+  }
 #pragma unroll 1
   for (int j = 0; j < 4; j++) {
     const int pr = 4 * g + j, rr = y0 + pr;
@@ -274,7 +453,7 @@ __global__ __launch_bounds__(256) void me_ssim_stats_kernel(SearchArgs p, SsimPl
         case 8: stats_at<8>(t, pr, c, B, &m, &v); break;
         default: stats_at<0>(t, pr, c, B, &m, &v); break;
       }
-    plane[(size_t)rr * s.pitch + x] = make_float2(m, sqrt_via_double(v));
+    put(rr, m, v);
   }
 }
 
@@ -359,7 +538,7 @@ __global__ __launch_bounds__(SSIM_THREADS) void me_ssim_kernel(SearchArgs p, int
     for (int t = tid; t < ng; t += nt) {
       const int cy = t / ngq, cx0 = (t - cy * ngq) * Q;
       const uint8_t* r = win + cy * ww + cx0;  // past the window: the launch's SSIM_PAD bytes
-      const float2* st = stats + (size_t)(wy0 + cy - pg.ylo) * pg.pitch;
+      const float2* st = stats + (size_t)(wy0 + cy - pg.ylo) * pg.ld;
       float fimr[Q], cv[Q];
 #pragma unroll
       for (int k = 0; k < Q; k++) {
@@ -400,7 +579,7 @@ __global__ __launch_bounds__(SSIM_THREADS) void me_ssim_kernel(SearchArgs p, int
       const int rp = staged ? ww : p.stride;
       const int lim = staged ? 0x7FFFFFFF : ww - 1 - cx0;
       auto rb = [&](int y, int x) -> float { return (float)r[y * rp + min(x, lim)]; };
-      const float2* st = stats + (size_t)(wy0 + cy - pg.ylo) * pg.pitch;
+      const float2* st = stats + (size_t)(wy0 + cy - pg.ylo) * pg.ld;
       float fimr[SSIM_QP], cv[SSIM_QP];
 #pragma unroll
       for (int k = 0; k < SSIM_QP; k++) {
@@ -527,24 +706,26 @@ __global__ __launch_bounds__(SSIM_THREADS) void me_ssim_kernel(SearchArgs p, int
 // span), and per candidate only the score's float operations in the
 // reference's order (ssim_key, as the float path) from the statistics plane's
 // mean and stddev.  The float path spent ~128 VALU per candidate on the chain.
+#ifndef ME_SSIM_ABL
+#define ME_SSIM_ABL 0  // A/B ablations (tools/dbg/ssim_variants.sh); 0 in the product
+#endif
 constexpr int SSIM_CREC = 48;                                // row record: 0^16, c ^ 0x7F, 0^16
 
 __host__ __device__ inline int ssim_mfma_lp(int S) { return 16 * ((2 * S + 15) / 16 + 3); }
 __host__ __device__ inline int ssim_mfma_rows(int S) { return 16 * ((2 * S + 1 + 15) / 16) + 15; }
 __host__ __device__ inline int ssim_mfma_lds(int S) {
-  return 256 + 16 * SSIM_CREC + ssim_mfma_rows(S) * ssim_mfma_lp(S);
+  return 16 * SSIM_CREC + ssim_mfma_rows(S) * ssim_mfma_lp(S);
 }
 
 // bh: the blocks' height -- 16, or the partial bottom row's H % 16 (its own
 // statistics plane; N = 16 bh pixels <= 256, so the identity above holds with
 // 256 -> N and 4161536 -> 16256 N; record rows >= bh are zero)
-__global__ __launch_bounds__(256) void me_ssim_mfma_kernel(SearchArgs p, int row0, int nbxf,
-                                                           const float2* stats, SsimPlane pg,
-                                                           int aligned16, int bh) {
+// Grid: the full rows' full-width blocks (plane 1), then the partial bottom
+// row's (plane 2, bh = H % 16), J's current-block statistics for each.
+__global__ __launch_bounds__(256) void me_ssim_mfma_kernel(SearchArgs p, SsimStatsJob J,
+                                                           int aligned16) {
   extern __shared__ __align__(16) uint8_t smem[];
   __shared__ uint64_t red[4];
-  __shared__ float cstat[2];
-  __shared__ int csum;
   typedef int v4i __attribute__((ext_vector_type(4)));
   typedef __attribute__((address_space(3))) const uint32_t lds_c32;
   typedef __attribute__((address_space(3))) const v4i lds_cv4i;
@@ -553,27 +734,41 @@ __global__ __launch_bounds__(256) void me_ssim_mfma_kernel(SearchArgs p, int row
   };
   const int tid = (int)threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n = lane & 15, hh = lane >> 4;
-  const int bx = (int)(blockIdx.x % (unsigned)nbxf), by = row0 + (int)(blockIdx.x / (unsigned)nbxf);
+  const int nbxf = J.nbxf;
+  // XCD-aware order: workgroup i runs on XCD i % 8, and XCD x takes a
+  // contiguous run of raster-order blocks, so the blocks sharing plane and
+  // window lines share that XCD's L2 (round robin sent horizontal neighbours
+  // to different XCDs: ~276 MB of plane reads from the Infinity cache at 1080p)
+  const int G = (int)gridDim.x, wg = (int)blockIdx.x;
+  const int xq = G >> 3, xr = G & 7, xcd = wg & 7, xk = wg >> 3;
+  const int blk = xcd < xr ? xcd * (xq + 1) + xk : xr * (xq + 1) + (xcd - xr) * xq + xk;
+  const int bx = blk % nbxf;
+  const int by = p.block_row_begin + blk / nbxf;
   const int S = p.range, W = p.width, H = p.height;
+  const int bh = min(16, H - 16 * by);
+  const int k = bh < 16 ? 2 : 1;
+  const float2* const stats = J.out[k];
+  const SsimPlane pg = J.pl[k];
+  // the block's mean, stddev and byte sum (me_ssim_stats_kernel)
+  const float4 cs = J.cst[blk];
   const int tlx = 16 * bx, tly = 16 * by;
   const int wx0 = max(tlx - S, 0), wy0 = max(tly - S, 0);
   const int ncx = min(tlx + S, W - 16) - wx0 + 1, ncy = min(tly + S, H - bh) - wy0 + 1;
   const int i0 = wx0 >> 4, ni = ((wx0 + ncx - 1) >> 4) - i0 + 1, nj = (ncy + 15) >> 4;
   const int LP = ssim_mfma_lp(S), R = 16 * nj + 15;
-  uint8_t* cblk = smem;                        // the block, raw
-  uint8_t* crec = smem + 256;                  // 16 row records
+  uint8_t* crec = smem;                        // 16 row records
   uint8_t* win = crec + 16 * SSIM_CREC;        // rows wy0 .., columns 16 i0 ..: r ^ 0x80
   for (int i = tid; i < 256; i += 256) {
     const int oy = i >> 4, ox = i & 15;
     const uint8_t c = oy < bh ? p.cur[(ptrdiff_t)(tly + oy - p.cur_row0) * p.stride + tlx + ox] : 0;
-    cblk[i] = c;
     crec[oy * SSIM_CREC + 16 + ox] = oy < bh ? c ^ 0x7F : 0;
     crec[oy * SSIM_CREC + ox] = 0;
     crec[oy * SSIM_CREC + 32 + ox] = 0;
   }
   // (columns and rows past the frame: zeros or the next bytes of the plane;
   // only masked candidates read them)
-  if (aligned16) {
+  if (ME_SSIM_ABL & 4) {
+  } else if (aligned16) {
     // 16-byte granules through a buffer resource over the resident rows
     // (reads past it return 0)
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -595,22 +790,7 @@ __global__ __launch_bounds__(256) void me_ssim_mfma_kernel(SearchArgs p, int row
     }
   }
   __syncthreads();
-  // the block's statistics (ssim.c:3-28 as the float path: one serial chain,
-  // wave 0) and byte sum
   const int N = 16 * bh;
-  if (tid < 64) {
-    float m0, v0;
-    patch_stats(cblk, 16, 16, bh, (float)N, &m0, &v0);
-    int cs = 0;
-    for (int i = lane; i < 256; i += 64) cs += cblk[i];  // rows >= bh: 0
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) cs += __shfl_xor(cs, off, 64);
-    if (tid == 0) {
-      cstat[0] = m0;
-      cstat[1] = v0;
-      csum = cs;
-    }
-  }
   // A fragments (me_band.hip's enter): lane (m = n, K group hh), fragment q =
   // bytes o .. o + 15 of record row 2 q + (hh >> 1), o = 16 + 16 (hh & 1) - m
   v4i A[8];
@@ -627,19 +807,43 @@ __global__ __launch_bounds__(256) void me_ssim_mfma_kernel(SearchArgs p, int row
       for (int e = 0; e < 4; e++) A[q][e] = (int)__builtin_amdgcn_alignbyte(d[e + 1], d[e], sh);
     }
   }
-  __syncthreads();
-  const float mp = cstat[0], sp = sqrt_via_double(cstat[1]);
-  // (int) mp = S1c / N: the rounded quotient stays below the next integer
-  // (1 - frac >= 1 / N is far above its ulp)
-  const int S1c = csum, imc = (int)mp;
+  const float mp = cs.x, sp = cs.y;
+  const float mp2 = __fmul_rn(mp, mp), sp2 = __fmul_rn(sp, sp);
+  // S1c: the block's byte sum; imc = (int) mp = S1c / N (the rounded quotient
+  // stays below the next integer: 1 - frac >= 1 / N is far above its ulp)
+  const int S1c = __float_as_int(cs.z), imc = (int)mp;
+  // S1r < 2^16, imr < 256: with ka = 127 - imc and kb = S1c - N imc (in [0, N))
+  // every factor fits v_mul_i32_i24
+  const int ka = 127 - imc, kb = S1c - N * imc;
   const int kc = 128 * S1c - 16256 * N;
   const float nf = (float)N, inv_nf = 1.0f / nf;  // exact when N is a power of two
   const bool pow2 = (N & (N - 1)) == 0;
   uint64_t best = ~0ull;
   const uint32_t xb0 = lds_addr(win) + (uint32_t)((n + (hh >> 1)) * LP + 16 * (hh & 1));
-#pragma unroll 1
-  for (int t = wave; t < ni * nj; t += 4) {
+  const int nt = ni * nj;
+  // the compact plane's entries of tile t's lane candidates: stddevs as one
+  // 16-byte load, byte sums as one 8-byte load (absolute columns 16 (i0 + ti)
+  // + 4 hh .. + 3, inside the padded row; masked candidates read row-clamped
+  // or padding entries, never used), loaded one tile ahead of their use
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
+  const float* sdp = reinterpret_cast<const float*>(stats);
+  const unsigned short* s1p = reinterpret_cast<const unsigned short*>(sdp + (size_t)pg.rows * pg.ld);
+  auto load_st = [&](int t, f4v* sd, u16x4* s1) {
     const int tj = t / ni, ti = t - tj * ni;
+    const size_t e = (size_t)(wy0 + min(16 * tj + n, ncy - 1) - pg.ylo) * pg.ld + 16 * (i0 + ti) + 4 * hh;
+    *sd = *reinterpret_cast<const f4v*>(sdp + e);
+    *s1 = *reinterpret_cast<const u16x4*>(s1p + e);
+  };
+  f4v nsd = {0.f, 0.f, 0.f, 0.f};
+  u16x4 ns1 = {0, 0, 0, 0};
+  if (!(ME_SSIM_ABL & 2) && wave < nt) load_st(wave, &nsd, &ns1);
+#pragma unroll 1
+  for (int t = wave; t < nt; t += 4) {
+    const int tj = t / ni, ti = t - tj * ni;
+    const f4v csd = nsd;
+    const u16x4 cs1 = ns1;
+    if (!(ME_SSIM_ABL & 2) && t + 4 < nt) load_st(t + 4, &nsd, &ns1);
     // B fragment q: window row 16 tj + n + 2 q + (hh >> 1), column 16 ti + 16 (hh & 1)
     const uint32_t xb = xb0 + (uint32_t)(16 * tj * LP + 16 * ti);
     v4i f[8];
@@ -647,23 +851,45 @@ __global__ __launch_bounds__(256) void me_ssim_mfma_kernel(SearchArgs p, int row
     for (int q = 0; q < 8; q++) f[q] = *reinterpret_cast<lds_cv4i*>((uintptr_t)(xb + (uint32_t)(2 * q * LP)));
     v4i acc = {0, 0, 0, 0};
 #pragma unroll
-    for (int q = 0; q < 8; q++) acc = MFMA16(A[q], f[q], acc, 0, 0, 0);
+    for (int q = 0; q < 8; q++) acc = (ME_SSIM_ABL & 8) ? acc + f[q] : MFMA16(A[q], f[q], acc, 0, 0, 0);
     // lane (n, hh): X of positions x = 16 (i0 + ti) + 4 hh + r, y = wy0 + 16 tj + n
     const int cy = 16 * tj + n, cx0 = 16 * (i0 + ti) + 4 * hh - wx0;
-    if (cy < ncy) {
-      const float2* st = stats + (size_t)(wy0 + cy - pg.ylo) * pg.pitch + wx0;
+    if (ME_SSIM_ABL & 3) {
+      uint64_t k = 0;
 #pragma unroll
-      for (int r = 0; r < 4; r++) {
-        const int cx = cx0 + r;
-        if (cx < 0 || cx >= ncx) continue;
-        const float2 v = st[cx];
-        // mean_r = fl(S1r / N): N mean_r is within N ulp / 2 < 1/2 of S1r
-        const int S1r = __float2int_rn(__fmul_rn(v.x, nf));
-        const int imr = (int)v.x;
-        const int cv = 127 * S1r + kc - acc[r] - imc * S1r - imr * S1c + N * imr * imc;
-        const float cvk = pow2 ? __fmul_rn((float)cv, inv_nf) : __fdiv_rn((float)cv, nf);
-        const uint64_t key = ssim_key(v.x, v.y, cvk, mp, sp, wx0 + cx - tlx, wy0 + cy - tly);
-        best = key < best ? key : best;
+      for (int r = 0; r < 4; r++) k += (uint32_t)acc[r] ^ __float_as_uint(csd[r]) ^ cs1[r];
+      best = k < best ? k : best;
+    } else {
+      // ssim.c:53-56 for the lane's four candidates, two per packed
+      // instruction (each half rounded as ssim_key's scalar operation)
+      const float C1 = 0.01f, C2 = 0.09f, C3 = 0.045f;  // ssim.c:48
+#pragma unroll
+      for (int h2 = 0; h2 < 2; h2++) {
+        f2v m, cvf;
+        const f2v sr = {csd[2 * h2], csd[2 * h2 + 1]};
+#pragma unroll
+        for (int e = 0; e < 2; e++) {
+          const int S1r = cs1[2 * h2 + e];
+          // the reference's mean: fl(S1r / N) (exact for N = 256); imr = (int) mean
+          m[e] = pow2 ? __fmul_rn((float)S1r, inv_nf) : __fdiv_rn((float)S1r, nf);
+          const int imr = (int)m[e];
+          // = 127 S1r + kc - X - imc S1r - imr S1c + N imr imc, 24-bit products
+          cvf[e] = (float)(__mul24(S1r, ka) + kc - acc[2 * h2 + e] - __mul24(imr, kb));
+        }
+        const f2v cvk = pow2 ? cvf * inv_nf : f2v{__fdiv_rn(cvf.x, nf), __fdiv_rn(cvf.y, nf)};
+        const f2v lum = div_rn2((2.f * m) * mp + C1, (m * m + mp2) + C1);
+        const f2v con = div_rn2((2.f * sr) * sp + C2, (sr * sr + sp2) + C2);
+        const f2v str = div_rn2(cvk + C3, sr * sp + C3);
+        const f2v score = (lum * con) * str;
+#pragma unroll
+        for (int e = 0; e < 2; e++) {
+          const int cx = cx0 + 2 * h2 + e;
+          const bool ok = cy < ncy && cx >= 0 && cx < ncx && score[e] > 0.f;
+          const uint64_t key = ((uint64_t)(0x7FFFFFFFu - __float_as_uint(score[e])) << 32) |
+                               ((uint32_t)(wy0 + cy - tly + 32768) << 16) |
+                               (uint32_t)(wx0 + cx - tlx + 32768);
+          best = ok && key < best ? key : best;
+        }
       }
     }
   }
@@ -698,64 +924,73 @@ hipError_t launch_ssim(const SearchArgs& p, hipStream_t stream) {
   if (cur + win + SSIM_PAD > GENERIC_LDS_BUDGET) win = 0;  // read the window from global memory
   // Patch statistics planes in the context scratch when it holds them
   // (attach_scratch sizes it with ssim_scratch); otherwise every block computes
-  // its own.  The full rows' plane first, then the partial bottom row's.
-  SsimPlane sp{0, 0, 0}, hp{0, 0, 0};
-  const float2* stats = nullptr;
-  const float2* hstats = nullptr;
+  // its own.  The full rows' plane, the partial bottom row's, then the current
+  // blocks' statistics for the matrix-core kernel -- all from one launch.
+  SsimStatsJob J{};
+  SsimPlane& sp = J.pl[1];
   int hbh = 0;
+  const float2* stats = nullptr;
+  bool hb = false;
   const size_t need = ssim_scratch(p);
   if (need && p.scratch && p.scratch_bytes >= need) {
     uint8_t* base = reinterpret_cast<uint8_t*>(p.scratch);
     if (ssim_plane(p, &sp)) {
-      float2* plane = reinterpret_cast<float2*>(base);
-      hipLaunchKernelGGL(me_ssim_stats_kernel, dim3((unsigned)((sp.pitch + 63) / 64),
-                                                    (unsigned)((sp.rows + 15) / 16)),
-                         dim3(256), 0, stream, p, sp, plane, B);
-      stats = plane;
+      J.out[1] = reinterpret_cast<float2*>(base);
+      J.ph[1] = B;
+      J.gy[1] = (sp.rows + 15) / 16;
+      stats = J.out[1];
       base += ssim_plane_bytes(sp);
     }
-    if (ssim_hb_plane(p, &hp, &hbh)) {
-      float2* plane = reinterpret_cast<float2*>(base);
-      hipLaunchKernelGGL(me_ssim_stats_kernel, dim3((unsigned)((hp.pitch + 63) / 64),
-                                                    (unsigned)((hp.rows + 15) / 16)),
-                         dim3(256), 0, stream, p, hp, plane, hbh);
-      hstats = plane;
+    if (ssim_hb_plane(p, &J.pl[2], &hbh)) {
+      J.out[2] = reinterpret_cast<float2*>(base);
+      J.ph[2] = hbh;
+      J.gy[2] = (J.pl[2].rows + 15) / 16;
+      base += ssim_plane_bytes(J.pl[2]);
+      hb = true;
     }
+    // 16 x 16 blocks, S <= 64: full-width columns on the matrix cores
+    J.nbxf = ssim_cur_stats_bytes(p) ? p.width / 16 : 0;
+    if (J.nbxf > 0) {
+      J.cst = reinterpret_cast<float4*>(base);
+      J.cst_n = rows * J.nbxf;
+      J.cur_a4 = p.stride % 4 == 0 && (uintptr_t)p.cur % 4 == 0;
+    }
+    const int gx = std::max((std::max(sp.pitch, J.pl[2].pitch) + 63) / 64, 1);
+    J.gy[0] = J.nbxf > 0 ? (J.cst_n + 256 * gx - 1) / (256 * gx) : 0;
+    hipLaunchKernelGGL(me_ssim_stats_kernel, dim3((unsigned)gx, (unsigned)(J.gy[0] + J.gy[1] + J.gy[2])),
+                       dim3(256), 0, stream, p, J);
   }
-  // 16 x 16 blocks with the statistics planes, S <= 64: the full-width columns
-  // on the matrix cores (full rows, then the partial bottom row with its own
-  // plane); the partial right column on the float path
-  const int a16 = p.stride % 16 == 0 && (uintptr_t)p.ref % 16 == 0 && p.ref_bytes > 0;
-  const int nbxf = B == 16 && p.range <= 64 ? p.width / 16 : 0;
+  // The matrix cores: the full rows (plane 1) and the partial bottom row (plane 2)
+  // of the full-width columns; the partial right column on the float path
   int r_full = 0;
-  if (stats && nbxf > 0) {
-    r_full = std::max(0, std::min(p.block_row_end, p.height / 16) - p.block_row_begin);
-    if (r_full > 0)
-      hipLaunchKernelGGL(me_ssim_mfma_kernel, dim3((unsigned)(r_full * nbxf)), dim3(256),
-                         ssim_mfma_lds(p.range), stream, p, p.block_row_begin, nbxf, stats, sp, a16,
-                         16);
+  const bool hb_mfma = hb && J.nbxf > 0;
+  if (J.nbxf > 0 && (stats || hb)) {
+    r_full = stats ? std::max(0, std::min(p.block_row_end, p.height / 16) - p.block_row_begin) : 0;
+    const int a16 = p.stride % 16 == 0 && (uintptr_t)p.ref % 16 == 0 && p.ref_bytes > 0;
+    const int nrow = r_full + (hb_mfma ? 1 : 0);
+    hipLaunchKernelGGL(me_ssim_mfma_kernel, dim3((unsigned)(nrow * J.nbxf)), dim3(256),
+                       ssim_mfma_lds(p.range), stream, p, J, a16);
   }
-  const bool hb_mfma = hstats && nbxf > 0;
-  if (hb_mfma)
-    hipLaunchKernelGGL(me_ssim_mfma_kernel, dim3((unsigned)nbxf), dim3(256), ssim_mfma_lds(p.range),
-                       stream, p, p.height / 16, nbxf, hstats, hp, a16, hbh);
+  const int nbxf = hb_mfma || r_full > 0 ? J.nbxf : 0;
+  // the float kernel reads only a float2 plane (a compact one serves the matrix cores)
+  const float2* fstats = sp.compact ? nullptr : stats;
   // + SSIM_PAD bytes: the last candidate group of the last row reads past the window
   const int lds = cur + (int)win + SSIM_PAD;
   if (r_full == 0 && !hb_mfma) {
     hipLaunchKernelGGL(me_ssim_kernel, dim3((unsigned)(rows * p.nbx)), dim3(SSIM_THREADS), lds, stream,
-                       p, p.block_row_begin, 0, (int)win, stats, sp);
+                       p, p.block_row_begin, 0, (int)win, fstats, sp);
   } else {
     // the rest: the partial right column of the full rows, then the partial
     // bottom row (its right-column block only when the row ran on the matrix cores)
     if (r_full > 0 && nbxf < p.nbx)
       hipLaunchKernelGGL(me_ssim_kernel, dim3((unsigned)(r_full * (p.nbx - nbxf))), dim3(SSIM_THREADS),
-                         lds, stream, p, p.block_row_begin, nbxf, (int)win, stats, sp);
+                         lds, stream, p, p.block_row_begin, nbxf, (int)win, fstats, sp);
     const int rb = p.block_row_begin + r_full;
     if (rb < p.block_row_end) {
       const int col0 = hb_mfma ? nbxf : 0;
       if (col0 < p.nbx)
         hipLaunchKernelGGL(me_ssim_kernel, dim3((unsigned)((p.block_row_end - rb) * (p.nbx - col0))),
-                           dim3(SSIM_THREADS), lds, stream, p, rb, col0, (int)win, stats, sp);
+                           dim3(SSIM_THREADS), lds, stream, p, rb, col0, (int)win, fstats, sp);
     }
   }
   return hipGetLastError();

@@ -1,0 +1,16 @@
+# Round 6: SSIM packed score epilogue + XCD-ordered blocks -- SSIM tests, then
+# A/B of the SSIM leg: previous commit, XCD order with the scalar epilogue, this build.
+set -e
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests/test_gpu_ssim.py tests/test_gpu_fuzz.py -x -q --timeout 300 --timeout-method thread > gpurun_out/r06r_pytest.log 2>&1
+O=gpurun_out/r06r_ssim_ab.jsonl
+: > $O
+for rep in 1 2; do
+  for lib in prev oldep cur; do
+    L=libme_hip_$lib.so; [ $lib = cur ] && L=libme_hip.so
+    ME_HIP_LIB=$L timeout -k 10 180 python3 bench.py --no-cpu --no-stream --no-4k --no-single --no-ssd --steps 10 --warmup 2 2>>gpurun_out/r06r_err.log | python3 -c "
+import json,sys; d=json.loads(sys.stdin.read()); s=d['ssim']
+print(json.dumps({'tag': '$lib', 'kernel_ms': s['kernel_ms'], 'parity': s['parity']['ok']}))" >> $O
+  done
+done
+cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof_r06r_ssim -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --no-cpu --no-stream --no-4k --no-single --no-ssd --steps 10 --warmup 2 > $GRAFT_REPO_ROOT/gpurun_out/r06r_prof.log 2>&1

@@ -84,7 +84,9 @@ times = trace_times()
 # optional passes (profile.sh SIZED=1): read requests by size, L2 hits / misses
 sized = {c: counter("*counter_collection.csv", c) for c in
          ("TCC_EA0_RDREQ_32B_sum", "TCC_EA0_RDREQ_64B_sum", "TCC_EA0_RDREQ_128B_sum",
-          "TCC_EA0_RDREQ_sum", "TCC_HIT_sum", "TCC_MISS_sum")}
+          "TCC_EA0_RDREQ_sum", "TCC_HIT_sum", "TCC_MISS_sum",
+          # profile.sh VALU=1: instruction counts (wave-level, all SQs)
+          "SQ_INSTS_VALU", "SQ_INSTS_MFMA", "SQ_INSTS_SALU", "SQ_WAVES")}
 summary = {}
 for r in stats:
     name = r.get("Name", "")
