@@ -57,6 +57,8 @@ struct Dev {
   bool searched = false;
   // Frame-pair pipeline (me_stream.hip), kept across calls.
   std::vector<uint8_t*> slots;        // device frames, slot_bytes each
+  std::vector<uint8_t*> slot_chunks;  // their allocations: kSlotChunk adjacent slots each
+  std::vector<uint8_t*> slot_spare;   // slots of the last chunk not handed out yet
   size_t slot_bytes = 0;
   uint8_t* stage[2] = {nullptr, nullptr};  // pinned staging for pageable frames
   hipEvent_t stage_ev[2] = {nullptr, nullptr};

@@ -7,9 +7,12 @@
 // pairs of frames/ForemanYF{1,2,4}) -- and keeps every device busy:
 //   - each frame is uploaded once per device, into a device slot that lives
 //     from the first to the last pair reading it;
-//   - pairs are searched in job-table launches (launch_jobs) of 1, 2, 4 and
-//     then 8 pairs: a launch's fill and drain are paid once per batch, and
-//     the first search starts after two uploads (profiles/r04h_*);
+//   - pairs are searched in job-table launches (launch_jobs) ramping 1, 2, 3,
+//     4, 6, 9 and then 12 pairs: a launch's fill and drain are paid once per
+//     batch, and the first search starts after two uploads (profiles/r04h_*);
+//   - uploads run one batch ahead of the searches, and a batch's frames that
+//     are adjacent in host memory and in their device slots go up in one
+//     copy (round 6);
 //   - uploads run on a copy stream, searches on the compute stream; the
 //     host-side staging and upload of pair n+1's new frame overlap the search
 //     of pair n (slots are reused oldest-freed first, so an upload never
@@ -45,8 +48,12 @@ std::mutex g_pin_mu;
 std::map<uintptr_t, size_t> g_pinned;  // me_host_alloc ranges: base -> bytes
 // Freed frame slots kept cooling before reuse (ME_STREAM_COOL overrides; tuning)
 static int cooling_slots() { return tuning().stream_cool > 0 ? tuning().stream_cool : 2; }
-// Pairs per search launch (ME_STREAM_BATCH overrides; tuning)
-constexpr int kPairBatch = 8;
+// Pairs per search launch after the ramp (ME_STREAM_BATCH overrides; tuning).
+// With uploads one batch ahead and merged copies, pinned 1080p pairs/s over two
+// sweeps: 8: 14.16k / 14.36k, 12: 14.42k / 14.50k, 16: 14.32k / 14.09k, 24:
+// 13.94k / 14.37k, 32: 14.13k / 14.27k (profiles/r06x_stream_batch.jsonl;
+// box noise ~2 %).  Round 5 (no lookahead): 8 was best.
+constexpr int kPairBatch = 12;
 constexpr int kEvRing = 16;  // batch events (Dev::upl_ev / batch_ev), ring by batch index
 }  // namespace
 
@@ -62,7 +69,9 @@ bool host_range_pinned(const void* p, size_t bytes) {
 void release_pipeline(Dev& d) {
   if (d.copy) (void)hipStreamSynchronize(d.copy);
   if (d.d2h) (void)hipStreamSynchronize(d.d2h);
-  for (size_t i = 0; i < d.slots.size(); i++) (void)hipFree(d.slots[i]);
+  for (size_t i = 0; i < d.slot_chunks.size(); i++) (void)hipFree(d.slot_chunks[i]);
+  d.slot_chunks.clear();
+  d.slot_spare.clear();
   for (int k = 0; k < kEvRing; k++) {
     if (d.upl_ev[k]) (void)hipEventDestroy(d.upl_ev[k]);
     if (d.batch_ev[k]) (void)hipEventDestroy(d.batch_ev[k]);
@@ -109,7 +118,9 @@ me_status prepare(me_ctx* c, Dev& d, size_t plane) {
   if (d.slot_bytes != plane) {  // frame size changed: drop the old slots
     HIPCHK(c, hipStreamSynchronize(d.stream));
     if (d.copy) HIPCHK(c, hipStreamSynchronize(d.copy));
-    for (size_t i = 0; i < d.slots.size(); i++) (void)hipFree(d.slots[i]);
+    for (size_t i = 0; i < d.slot_chunks.size(); i++) (void)hipFree(d.slot_chunks[i]);
+    d.slot_chunks.clear();
+    d.slot_spare.clear();
     d.slots.clear();
     d.slot_bytes = plane;
   }
@@ -137,11 +148,23 @@ me_status upload_pinned(me_ctx* c, Dev& d, uint8_t* dst, const uint8_t* src, int
   return ME_OK;
 }
 
+// Slots are allocated kSlotChunk at a time, adjacent in one allocation, and
+// handed out (and, being freed in upload order, reused) in address order, so
+// a batch's new frames mostly land in adjacent slots: frames adjacent in host
+// memory too then go up in one copy (upload_batch).
+constexpr int kSlotChunk = 8;
+
 me_status new_slot(me_ctx* c, Dev& d, int* idx) {
-  uint8_t* p = nullptr;
-  if (hipMalloc((void**)&p, d.slot_bytes) != hipSuccess)
-    return fail(c, ME_ENOMEM, "hipMalloc(%zu) for a frame slot failed", d.slot_bytes);
-  d.slots.push_back(p);
+  if (d.slot_spare.empty()) {
+    uint8_t* p = nullptr;
+    if (hipMalloc((void**)&p, d.slot_bytes * kSlotChunk) != hipSuccess)
+      return fail(c, ME_ENOMEM, "hipMalloc(%zu) for %d frame slots failed", d.slot_bytes * kSlotChunk,
+                  kSlotChunk);
+    d.slot_chunks.push_back(p);
+    for (int k = kSlotChunk - 1; k >= 0; k--) d.slot_spare.push_back(p + (size_t)k * d.slot_bytes);
+  }
+  d.slots.push_back(d.slot_spare.back());
+  d.slot_spare.pop_back();
   *idx = (int)d.slots.size() - 1;
   return ME_OK;
 }
@@ -269,9 +292,13 @@ me_status run_pairs(me_ctx* c, Dev& d, const Job& j, int p0, int p1) {
   // Pairs are searched G at a time in one job-table launch (launch_jobs: the
   // flow / item kernels' job tables, SSD pairs sharing the matrix cores'
   // launches), so a launch's fill and drain are paid once per G pairs.  The
-  // slots a batch frees cool while the next batch's frames upload into older
-  // ones: at least G + 1 of them.
-  const size_t cool = (size_t)std::max(cooling_slots(), G + 1);
+  // slots a batch frees cool while later batches' frames upload into older
+  // ones.  Uploads run one batch ahead (below): batch b + 1's are enqueued when
+  // the host has waited for batch b - 2, so the slots they reuse must have been
+  // freed by batch b - 2 or earlier -- two batches' worth cooling, at least
+  // 2 G + 1 (with G + 1, most reused slots were batch b - 1's, and the copy
+  // queue waited for that search before uploading).
+  const size_t cool = (size_t)std::max(cooling_slots(), 2 * G + 1);
   // Ordering events: one per batch on each stream, not one per frame slot.
   // The round-3 scheme (a ready event per upload, a free event per released
   // slot, one wait per frame of every pair) put ~13 event packets between two
@@ -282,31 +309,56 @@ me_status run_pairs(me_ctx* c, Dev& d, const Job& j, int p0, int p1) {
   int synced = -1;  // newest batch the host has waited for
   std::vector<SearchJob> jobs;
   jobs.reserve((size_t)G);
-  int batch = 0;
   // Batches ramp up 1, 2, 3, 4, 6, then G pairs: the first search starts after
   // two uploads instead of G + 1.  A batch's new frames upload while the batch
   // before it searches, and one upload (42 us at 1080p) is 0.6-0.7 of a pair's
   // search, so batches may grow by about 1.5x: doubling left the GPU idle
   // 27, 55 and 128 us before the 2-, 4- and 8-pair searches (profiles/r04m_*).
-  for (int n0 = p0, gb = 1; n0 < p1; n0 += gb, gb = std::min(gb + std::max(1, gb / 2), G), batch++) {
+  std::vector<std::pair<int, int>> sched;  // pairs [n0, n1) of each batch
+  for (int n0 = p0, gb = 1; n0 < p1; n0 += gb, gb = std::min(gb + std::max(1, gb / 2), G)) {
     if (tuning().stream_ramp == 0) gb = G;  // tuning build: fixed batches (the round-3 behaviour)
-    const int n1 = std::min(p1, n0 + gb);
-    if (kAhead <= 8 && batch >= kAhead) {
-      HIPCHK(c, hipEventSynchronize(d.batch_ev[(batch - kAhead) % kEvRing]));
-      synced = batch - kAhead;
+    sched.emplace_back(n0, std::min(p1, n0 + gb));
+  }
+  const int nsched = (int)sched.size();
+  // Uploads run one batch ahead of the searches (round 6): batch b + 1's new
+  // frames are enqueued on the copy stream together with batch b's search, so
+  // by the time batch b + 1's search is enqueued (the host waits for batch
+  // b - 1 first) they have usually landed, and the host, seeing their event
+  // complete, enqueues the search with no wait packet on the compute queue.
+  // The wait packets were the launch gaps: 18.5 us between launches, and
+  // 14.8-15.0k instead of 14.0k pinned pairs/s without them
+  // (profiles/r05zz6_stream_wait_experiments.txt).
+  std::vector<char> has_upl((size_t)nsched, 0);
+  // pinned frames of a batch whose slots and host rows are both adjacent go up
+  // in one copy: 2 MB copies ran at 44.7 GB/s against 49.9 for large ones
+  // (profiles/r03bp_h2d_probe.txt), ~10 us between back-to-back copies
+  // (profiles/r06u_*), and the ramp's growth is bound by the upload rate
+  // (one copy never spans two allocations: the slots of one chunk, host rows
+  // inside one me_host_alloc range -- adjacent addresses alone are not enough)
+  uint8_t* run_dst = nullptr;
+  const uint8_t* run_src = nullptr;
+  size_t run_n = 0;
+  int run_si = -1;
+  auto flush_run = [&]() -> me_status {
+    if (run_n) {
+      me_status st;
+      if ((st = upload_pinned(c, d, run_dst, run_src, W, (int)(H * run_n), W)) != ME_OK) return st;
     }
-    jobs.clear();
-    me::SearchArgs base{};
+    run_n = 0;
+    return ME_OK;
+  };
+  auto upload_batch = [&](int bi) -> me_status {
     int uploads = 0;
-    for (int n = n0; n < n1; n++) {
+    for (int n = sched[bi].first; n < sched[bi].second; n++) {
       for (int side = 0; side < 2; side++) {
         const int f = j.pairs[2 * n + side];
         if (slot_of[f] >= 0) continue;
         // Keep freed slots cooling: reusing a slot the previous batch just
         // released would serialise this upload behind that search.
         int si;
+        me_status st;
         if (free_slots.size() < cool) {
-          if ((s = new_slot(c, d, &si)) != ME_OK) return s;
+          if ((st = new_slot(c, d, &si)) != ME_OK) return st;
           last_batch.push_back(-1);
         } else {
           si = free_slots.front();
@@ -318,20 +370,34 @@ me_status run_pairs(me_ctx* c, Dev& d, const Job& j, int p0, int p1) {
         }
         const uint8_t* src = j.frames[f];
         if (host_range_pinned(src, span)) {
-          if ((s = upload_pinned(c, d, d.slots[si], src, W, H, j.stride)) != ME_OK) return s;
+          if (j.stride != W) {
+            if ((st = flush_run()) != ME_OK) return st;
+            if ((st = upload_pinned(c, d, d.slots[si], src, W, H, j.stride)) != ME_OK) return st;
+          } else if (run_n && si == run_si + (int)run_n && si / kSlotChunk == run_si / kSlotChunk &&
+                     d.slots[si] == run_dst + run_n * plane && src == run_src + run_n * plane &&
+                     host_range_pinned(run_src, (run_n + 1) * plane)) {
+            run_n++;
+          } else {
+            if ((st = flush_run()) != ME_OK) return st;
+            run_dst = d.slots[si];
+            run_src = src;
+            run_si = si;
+            run_n = 1;
+          }
         } else {
-          if ((s = ensure_staging(c, d, plane)) != ME_OK) return s;
+          if ((st = flush_run()) != ME_OK) return st;
+          if ((st = ensure_staging(c, d, plane)) != ME_OK) return st;
           // the copy that last read this staging buffer must be done
           HIPCHK(c, hipEventSynchronize(d.stage_ev[stage_k]));
-          uint8_t* st = d.stage[stage_k];
+          uint8_t* stg = d.stage[stage_k];
           // The copy into staging is host-memory-bound on one thread (a 1080p
           // frame ~80 us, more than a pair's search): split it over the caller
           // and kCpy - 1 helper threads.
           auto copy_rows = [&](int y0, int y1) {
             if (j.stride == W)
-              memcpy(st + (size_t)y0 * W, src + (size_t)y0 * W, (size_t)(y1 - y0) * W);
+              memcpy(stg + (size_t)y0 * W, src + (size_t)y0 * W, (size_t)(y1 - y0) * W);
             else
-              for (int y = y0; y < y1; y++) memcpy(st + (size_t)y * W, src + (size_t)y * j.stride, W);
+              for (int y = y0; y < y1; y++) memcpy(stg + (size_t)y * W, src + (size_t)y * j.stride, W);
           };
           const int kCpy = std::min(tuning().stream_cpy > 0 ? tuning().stream_cpy : 4, std::max(1, H / 64));
           if (kCpy > 1 && !d.stage_pool) {
@@ -345,13 +411,37 @@ me_status run_pairs(me_ctx* c, Dev& d, const Job& j, int p0, int p1) {
             d.stage_pool->run_split(kCpy, [&](int i) { copy_rows(H * i / kCpy, H * (i + 1) / kCpy); });
           else
             copy_rows(0, H);
-          if ((s = upload_pinned(c, d, d.slots[si], st, W, H, W)) != ME_OK) return s;
+          if ((st = upload_pinned(c, d, d.slots[si], stg, W, H, W)) != ME_OK) return st;
           HIPCHK(c, hipEventRecord(d.stage_ev[stage_k], d.copy));
           stage_k ^= 1;
         }
         uploads++;
         slot_of[f] = si;
       }
+    }
+    {
+      const me_status st = flush_run();
+      if (st != ME_OK) return st;
+    }
+    // one event for this batch's uploads (the copy stream is in order: frames
+    // uploaded by earlier batches are covered by their batches' events)
+    if (uploads) {
+      HIPCHK(c, hipEventRecord(d.upl_ev[bi % kEvRing], d.copy));
+      has_upl[bi] = 1;
+    }
+    return ME_OK;
+  };
+  int batch = 0;
+  for (; batch < nsched; batch++) {
+    const int n0 = sched[batch].first, n1 = sched[batch].second;
+    if (kAhead <= 8 && batch >= kAhead) {
+      HIPCHK(c, hipEventSynchronize(d.batch_ev[(batch - kAhead) % kEvRing]));
+      synced = batch - kAhead;
+    }
+    if (batch == 0 && (s = upload_batch(0)) != ME_OK) return s;
+    jobs.clear();
+    me::SearchArgs base{};
+    for (int n = n0; n < n1; n++) {
       const int sr = slot_of[j.pairs[2 * n]], sc = slot_of[j.pairs[2 * n + 1]];
       const size_t o = (size_t)(n - p0) * nb;
       if (n == n0)
@@ -359,18 +449,24 @@ me_status run_pairs(me_ctx* c, Dev& d, const Job& j, int p0, int p1) {
                          out_mv + 2 * o, out_cost + o);
       jobs.push_back(SearchJob{d.slots[sr], 0, d.slots[sc], 0, 0, nby, out_mv + 2 * o, out_cost + o});
     }
-    // one wait for this batch's uploads (the copy stream is in order: frames
-    // uploaded by earlier batches were covered by their batches' waits)
-    if (uploads) {
-      HIPCHK(c, hipEventRecord(d.upl_ev[batch % kEvRing], d.copy));
-      HIPCHK(c, hipStreamWaitEvent(d.stream, d.upl_ev[batch % kEvRing], 0));
+    // this batch's uploads: a wait packet only if they have not landed yet
+    if (has_upl[batch]) {
+      const hipError_t q = hipEventQuery(d.upl_ev[batch % kEvRing]);
+      if (q == hipErrorNotReady)
+        HIPCHK(c, hipStreamWaitEvent(d.stream, d.upl_ev[batch % kEvRing], 0));
+      else if (q != hipSuccess)
+        return fail(c, ME_EDEVICE, "upload event: %s", hipGetErrorString(q));
     }
-    while (!own_dl && downloaded < batch)  // the previous batch's records, behind these uploads
-      if ((s = download()) != ME_OK) return s;
     if ((s = me::attach_scratch(c, d, base, false, n1 - n0)) != ME_OK) return s;
     if ((s = me::launch_jobs_ordered(c, d, base, jobs.data(), n1 - n0, d.stream)) != ME_OK) return s;
     HIPCHK(c, hipEventRecord(d.batch_ev[batch % kEvRing], d.stream));
     ranges.emplace_back(n0, n1);
+    // then the next batch's uploads (after the launch: pageable frames' host
+    // copies into staging must not hold back this search's enqueue), then the
+    // previous batch's records behind them on the copy stream
+    if (batch + 1 < nsched && (s = upload_batch(batch + 1)) != ME_OK) return s;
+    while (!own_dl && downloaded < batch)
+      if ((s = download()) != ME_OK) return s;
     if (own_dl && (s = download()) != ME_OK) return s;
     // Move the records of batches the host already waited for (their downloads
     // are done or nearly), and never let the event ring wrap.
