@@ -298,7 +298,9 @@ me_status run_pairs(me_ctx* c, Dev& d, const Job& j, int p0, int p1) {
   // freed by batch b - 2 or earlier -- two batches' worth cooling, at least
   // 2 G + 1 (with G + 1, most reused slots were batch b - 1's, and the copy
   // queue waited for that search before uploading).
-  const size_t cool = (size_t)std::max(cooling_slots(), 2 * G + 1);
+  // (tuning build: ME_STREAM_UPL = U batches ahead needs (U + 1) G + 1)
+  const int U = tuning().stream_upl > 0 ? tuning().stream_upl : 1;
+  const size_t cool = (size_t)std::max(cooling_slots(), (U + 1) * G + 1);
   // Ordering events: one per batch on each stream, not one per frame slot.
   // The round-3 scheme (a ready event per upload, a free event per released
   // slot, one wait per frame of every pair) put ~13 event packets between two
@@ -438,7 +440,9 @@ me_status run_pairs(me_ctx* c, Dev& d, const Job& j, int p0, int p1) {
       HIPCHK(c, hipEventSynchronize(d.batch_ev[(batch - kAhead) % kEvRing]));
       synced = batch - kAhead;
     }
-    if (batch == 0 && (s = upload_batch(0)) != ME_OK) return s;
+    if (batch == 0)
+      for (int u = 0; u < U && u < nsched; u++)
+        if ((s = upload_batch(u)) != ME_OK) return s;
     jobs.clear();
     me::SearchArgs base{};
     for (int n = n0; n < n1; n++) {
@@ -464,7 +468,7 @@ me_status run_pairs(me_ctx* c, Dev& d, const Job& j, int p0, int p1) {
     // then the next batch's uploads (after the launch: pageable frames' host
     // copies into staging must not hold back this search's enqueue), then the
     // previous batch's records behind them on the copy stream
-    if (batch + 1 < nsched && (s = upload_batch(batch + 1)) != ME_OK) return s;
+    if (batch + U < nsched && (s = upload_batch(batch + U)) != ME_OK) return s;
     while (!own_dl && downloaded < batch)
       if ((s = download()) != ME_OK) return s;
     if (own_dl && (s = download()) != ME_OK) return s;
