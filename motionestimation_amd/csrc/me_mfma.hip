@@ -60,6 +60,12 @@ constexpr int MFMA_DLY = 1;
 #ifndef SSD8_STRIP
 #define SSD8_STRIP 32  // 8x8 kernel: tile columns per strip of the workgroup order (1,024 pixels)
 #endif
+#ifndef ME_SSD8_ABL
+#define ME_SSD8_ABL 0  // A/B ablations of the 8x8 kernel (1: no steps, 2: no re-staging); 0 in the product
+#endif
+#ifndef ME_SSD8_S2PERM
+#define ME_SSD8_S2PERM 1  // 8x8: S2 table rows permuted in LDS (bank-conflict-free reads)
+#endif
 #ifndef ME_SSD8_WP
 #define ME_SSD8_WP 80  // 8x8 window copy pitch: 4 x (L + 8 = 56) x 80 + S2 table (L + 1) x 256 = 30 KB at L = 48
 #endif
@@ -724,10 +730,27 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd8_kernel(SearchArgs p, M
       }
     }
     const int sbase = ((y0 - g.ya0) * g.pitch + xa + 64 * gx) * 4;
+#if ME_SSD8_S2PERM
+    // S2 rows permuted in LDS: position p of the group at dword (p & 3) 16 +
+    // (p >> 2), so the 16 positions 4 n + s one wave reads per step are 16
+    // adjacent banks (in order, p = 4 n + s sat on banks 4 n + s: n and n + 8
+    // collided, a 2-way conflict on every step's S2 read).  One wave-wide
+    // 4-byte LDS DMA per row: lane i lands at dword i and loads position
+    // 4 (i & 15) + (i >> 4) -- the row's 256 bytes, read once.
+    {
+      const int t = opaque(tid), ln = t & 63, wv = t >> 6;
+      const uint32_t src = (uint32_t)(sbase + 4 * (4 * (ln & 15) + (ln >> 4)));
+      for (int rho = wv; rho < L; rho += 4)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rs2, (__attribute__((address_space(3))) void*)(s2t + rho * RB), 4,
+            src + (uint32_t)(rho * g.pitch * 4), 0, 0, 0);
+    }
+#else
     dma16(rs2, s2t, L * RB, [&](int d) {
       const int rho = d / RB, k = d - rho * RB;
       return (uint32_t)(sbase + rho * g.pitch * 4 + k);
     });
+#endif
   };
   auto shift_copies = [&]() {
     typedef __attribute__((address_space(3))) uint32_t lds_w32;
@@ -800,7 +823,8 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd8_kernel(SearchArgs p, M
   const uint32_t lbase = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) uint8_t*)smem);
   const uint32_t lds_lane = lbase + (uint32_t)(sig * COPY + 2 * h * WP + ccol);
   const uint32_t s2t_lane = (uint32_t)(uintptr_t)(
-      (__attribute__((address_space(3))) uint8_t*)s2t) + (uint32_t)(4 * n + s) * 4u;
+      (__attribute__((address_space(3))) uint8_t*)s2t) +
+      (uint32_t)(ME_SSD8_S2PERM ? 16 * s + n : 4 * n + s) * 4u;
   typedef __attribute__((address_space(3))) const int lds_i32;
 
   for (; gx < ngx; gx++) {
@@ -817,7 +841,7 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd8_kernel(SearchArgs p, M
   }
   for (int ch = 0; ch < nch; ch++) {
     const int y0 = ya + ch * L;
-    if (ch > 0 || gx > 0) {
+    if (!(ME_SSD8_ABL & 2) && (ch > 0 || gx > 0)) {
       __syncthreads();
       stage(y0);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -889,7 +913,8 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd8_kernel(SearchArgs p, M
       const int tly = tly0 + 8 * hh;
       full = full && max(tly - S, 0) <= y0 && min(tly + S, H - 8) >= y0 + L - 1;
     }
-    if (full) body(std::false_type{});
+    if (ME_SSD8_ABL & 1) {
+    } else if (full) body(std::false_type{});
     else body(std::true_type{});
 #pragma unroll
     for (int r = 0; r < 4; r++) {
