@@ -63,6 +63,9 @@ constexpr int MFMA_DLY = 1;
 #ifndef ME_SSD8_ABL
 #define ME_SSD8_ABL 0  // A/B ablations of the 8x8 kernel (1: no steps, 2: no re-staging); 0 in the product
 #endif
+#ifndef ME_SSD8_NT
+#define ME_SSD8_NT 2  // 8x8: horizontally adjacent 4x4-block tiles per workgroup (1 or 2)
+#endif
 #ifndef ME_SSD8_S2PERM
 #define ME_SSD8_S2PERM 1  // 8x8: S2 table rows permuted in LDS (bank-conflict-free reads)
 #endif
@@ -648,10 +651,16 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd16_kernel(SearchArgs p, 
 //   key = ((S2 + 1) << 6) + (y - y0) + (acc << 7) = (SSD - p + 1) << 6 | (y - y0)
 // SSD <= 64 * 255^2 < 2^22, so valid keys < 2^28; x out of window: acc + 2^22
 // (keys in [2^29, 2^30)); y out of window: bit 31.  Chunks of L = 16 KM8 rows (48).
-// Workgroup = one tile, 4 waves (phase s), walking the tile's groups of 64
-// candidate columns one after another: the (cost, dy, dx) keys meet in LDS and
-// leave once, with no cross-workgroup merge (per-group workgroups merged through
-// device-scope atomics that reach memory: 35 MB of the 8K search's writes).
+// Workgroup = NT horizontally adjacent tiles (ME_SSD8_NT), 4 waves (phase s),
+// walking the union of the tiles' groups of 64 candidate columns one after
+// another: the (cost, dy, dx) keys meet in LDS and leave once, with no
+// cross-workgroup merge (per-group workgroups merged through device-scope
+// atomics that reach memory: 35 MB of the 8K search's writes).  Round 6: two
+// tiles share every staged window row and S2 row and every B fragment -- one
+// MFMA per tile per step on the same f -- so the staging (L2 / Infinity-cache
+// reads of window and S2, the copy pass, the barriers: 44 of 107 ms per 16 8K
+// frames with the steps switched off) is paid once per two tiles; their
+// candidate ranges overlap in all but 32 columns.
 template <int KM8>
 __global__ __launch_bounds__(256)
 __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd8_kernel(SearchArgs p, MfmaGeom g) {
@@ -661,17 +670,19 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd8_kernel(SearchArgs p, M
   constexpr int COPY = CROWS * WP;
   constexpr int RB = 256;          // bytes per S2 table row (L + 1 rows: one prefetch past)
   static_assert(L <= 64, "6-bit row index");
+  constexpr int NT = ME_SSD8_NT;   // tiles per workgroup
+  static_assert(NT >= 1 && NT <= 4, "1 to 4 tiles per workgroup");
   extern __shared__ __align__(16) uint8_t smem[];
-  unsigned long long* keys = reinterpret_cast<unsigned long long*>(smem + 4 * COPY);
-  int* cc = reinterpret_cast<int*>(smem + 4 * COPY + 16 * 8);
-  uint8_t* s2t = smem + 4 * COPY + 16 * 8 + 16 * 4;  // [L][64] ints
+  unsigned long long* keys = reinterpret_cast<unsigned long long*>(smem + 4 * COPY);  // [NT][16]
+  int* cc = reinterpret_cast<int*>(smem + 4 * COPY + 16 * NT * 8);                     // [NT][16]
+  uint8_t* s2t = smem + 4 * COPY + 16 * NT * 12;  // [L][64] ints
   constexpr int QW = WP / 16;                        // 16-byte granules per copy row
   uint8_t* nxt = s2t + (L + 1) * RB;                 // [CROWS][QW] words: the 4 bytes after each granule
 
   const int tid = (int)threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n = lane & 15, h = lane >> 4;
   const int S = p.range, W = p.width, H = p.height;
-  int tile;
+  int wcol, ty;  // the workgroup's column of NT tiles, its tile row
   {
     // Workgroups in vertical strips of SSD8_STRIP tile columns, each strip
     // walked down its tile rows (then across the strip, then the groups); each
@@ -682,18 +693,30 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd8_kernel(SearchArgs p, M
     const int nwg = (int)gridDim.x, bid = (int)blockIdx.x;
     const int x = bid & 7, m = bid >> 3, q = nwg >> 3, rem = nwg & 7;
     const int lin = x * q + min(x, rem) + m;
-    const int sw = min(SSD8_STRIP, g.tiles_x);
+    const int wcols = (g.tiles_x + NT - 1) / NT;
+    const int sw = min(SSD8_STRIP / NT, wcols);
     const int per_strip = g.tiles_y * sw;
     const int st = lin / per_strip, r = lin - st * per_strip;
-    const int sws = min(sw, g.tiles_x - st * sw);  // the last strip may be narrower
-    const int ty = r / sws, txl = r - ty * sws;
-    tile = ty * g.tiles_x + st * sw + txl;
+    const int sws = min(sw, wcols - st * sw);  // the last strip may be narrower
+    ty = r / sws;
+    wcol = st * sw + (r - ty * sws);
   }
-  const int tx = tile % g.tiles_x, ty = tile / g.tiles_x;
-  const int bc0 = 4 * tx, br0 = g.row0 + 4 * ty;
-  const int nbc = min(4, g.nbx - bc0), nbr = min(4, g.row0 + g.nrows - br0);
-  const int tlx0 = 8 * bc0, tly0 = 8 * br0;
-  const int xa = max(tlx0 - S, 0), xb = min(tlx0 + 8 * (nbc - 1) + S, W - 8);
+  // tile k of the workgroup: tile column NT wcol + k (none past the last)
+  int bc0[NT], nbc[NT], tlx0[NT];
+#pragma unroll
+  for (int k = 0; k < NT; k++) {
+    bc0[k] = 4 * (NT * wcol + k);
+    nbc[k] = NT * wcol + k < g.tiles_x ? min(4, g.nbx - bc0[k]) : 0;
+    tlx0[k] = 8 * bc0[k];
+  }
+  int kl = 0;  // the last tile present
+#pragma unroll
+  for (int k = 1; k < NT; k++)
+    if (nbc[k] > 0) kl = k;
+  const int br0 = g.row0 + 4 * ty;
+  const int nbr = min(4, g.row0 + g.nrows - br0);
+  const int tly0 = 8 * br0;
+  const int xa = max(tlx0[0] - S, 0), xb = min(tlx0[kl] + 8 * (nbc[kl] - 1) + S, W - 8);
   const int ya = max(tly0 - S, 0), yb = min(tly0 + 8 * (nbr - 1) + S, H - 8);
   const int ngx = (xb - xa + 1 + 63) >> 6;  // groups of 64 positions this tile needs
   const int nch = (yb - ya + 1 + L - 1) / L;
@@ -776,33 +799,34 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd8_kernel(SearchArgs p, M
     }
   };
 
-  if (tid < 16) {
+  if (tid < 16 * NT) {
     keys[tid] = ~0ull;
     cc[tid] = 0;
   }
   stage(ya);
   __syncthreads();
-  // A fragment: lane (n, h) holds block n's rows 2h, 2h+1 as c'' = c ^ 0x7F
-  v4i a;
-  {
+  // A fragments: lane (n, h) holds block n's rows 2h, 2h+1 of each tile as c'' = c ^ 0x7F
+  v4i a[NT];
+#pragma unroll
+  for (int k = 0; k < NT; k++) {
     const int br = n >> 2, bc = n & 3;
-    const bool present = br < nbr && bc < nbc;
+    const bool present = br < nbr && bc < nbc[k];
     v4i v = {0, 0, 0, 0};
     if (present) {
-      const uint8_t* row = p.cur + (ptrdiff_t)(tly0 + 8 * br + 2 * h - p.cur_row0) * p.stride + tlx0 + 8 * bc;
+      const uint8_t* row = p.cur + (ptrdiff_t)(tly0 + 8 * br + 2 * h - p.cur_row0) * p.stride + tlx0[k] + 8 * bc;
       const uint32_t* r0 = reinterpret_cast<const uint32_t*>(row);
       const uint32_t* r1 = reinterpret_cast<const uint32_t*>(row + p.stride);
       v[0] = (int)(r0[0] ^ 0x7F7F7F7Fu); v[1] = (int)(r0[1] ^ 0x7F7F7F7Fu);
       v[2] = (int)(r1[0] ^ 0x7F7F7F7Fu); v[3] = (int)(r1[1] ^ 0x7F7F7F7Fu);
     }
-    a = v;
+    a[k] = v;
     int part = 0;
 #pragma unroll
     for (int e = 0; e < 4; e++) {
       part = __builtin_amdgcn_sdot4(v[e], v[e], part, false);
       part = __builtin_amdgcn_sdot4(v[e], 0x02020202, part, false);
     }
-    if (wave == 0 && present) atomicAdd(&cc[n], part);
+    if (wave == 0 && present) atomicAdd(&cc[16 * k + n], part);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -830,15 +854,17 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd8_kernel(SearchArgs p, M
   for (; gx < ngx; gx++) {
   X0 = (xa + 64 * gx) & ~3;
   const int xn = xa + 64 * gx + 4 * n + s;
-  v4i initv;
+  v4i initv[NT];
 #pragma unroll
-  for (int r = 0; r < 4; r++) {
-    const int tlx = tlx0 + 8 * r;
-    const int dx = xn - tlx;
-    const bool ok = r < nbc && dx >= max(-S, -tlx) && dx <= min(S, W - 8 - tlx);
-    const int c = cc[4 * h + r];
-    initv[r] = ok ? (c >> 1) : (c >> 1) + (1 << 22);
-  }
+  for (int k = 0; k < NT; k++)
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const int tlx = tlx0[k] + 8 * r;
+      const int dx = xn - tlx;
+      const bool ok = r < nbc[k] && dx >= max(-S, -tlx) && dx <= min(S, W - 8 - tlx);
+      const int c = cc[16 * k + 4 * h + r];
+      initv[k][r] = ok ? (c >> 1) : (c >> 1) + (1 << 22);
+    }
   for (int ch = 0; ch < nch; ch++) {
     const int y0 = ya + ch * L;
     if (!(ME_SSD8_ABL & 2) && (ch > 0 || gx > 0)) {
@@ -849,7 +875,11 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd8_kernel(SearchArgs p, M
       shift_copies();
       __syncthreads();
     }
-    uint32_t best[4] = {~0u, ~0u, ~0u, ~0u};
+    uint32_t best[NT][4];
+#pragma unroll
+    for (int k = 0; k < NT; k++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) best[k][r] = ~0u;
     uint32_t lp = lds_lane, sp = s2t_lane;
     // One window row (8 bytes at x_n) of lane group h: window row row + 2h.  Step
     // t's fragment is rows t + 2h, t + 2h + 1, so consecutive steps share a row:
@@ -867,19 +897,23 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd8_kernel(SearchArgs p, M
     // Keys of one step; steps pair up into one v_min3 per block.  MASKED = false
     // on chunks where every lane group's block row is valid for every row
     // (the middle of a tile's range): no y test at all.
-    auto keys_of = [&](int yrel, const v4i& av, int s2v, uint32_t (&k)[4], auto MASKED) {
+    // (the position term Pf is the same for every tile: S2 is the window's)
+    auto pos_term = [&](int yrel, int s2v, auto MASKED) -> uint32_t {
       uint32_t Pf = lshl6_add((uint32_t)s2v, (uint32_t)(64 + yrel));
       if constexpr (decltype(MASKED)::value) {
         const uint32_t Wd = sad_u32((uint32_t)(2 * (y0 + yrel)), sumLH, Cv);
         Pf = (Wd & 0x80000000u) | Pf;
       }
+      return Pf;
+    };
+    auto keys_of = [&](const v4i& av, uint32_t Pf, uint32_t (&k)[4]) {
 #pragma unroll
       for (int r = 0; r < 4; r++) k[r] = ((uint32_t)av[r] << 7) + Pf;
     };
     auto body = [&](auto MASKED) {
       v2i rw[3];  // window rows t+2h (older), t+2h+1, and the prefetched t+2h+2
       int sv[2];
-      uint32_t kp[4];
+      uint32_t kp[NT][4];
       load_row(rw[0], std::integral_constant<int, 0>{});
       load_row(rw[1], std::integral_constant<int, 1>{});
       sv[0] = *reinterpret_cast<lds_i32*>((uintptr_t)sp);
@@ -895,14 +929,20 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd8_kernel(SearchArgs p, M
           sv[(t + 1) & 1] = *reinterpret_cast<lds_i32*>((uintptr_t)(sp + (uint32_t)(t + 1) * RB));
         const v2i r0 = rw[t % 3], r1 = rw[(t + 1) % 3];
         const v4i f = {r0[0], r0[1], r1[0], r1[1]};
-        const v4i acc = MFMA16(a, f, initv, 0, 0, 0);
-        if constexpr ((t & 1) == 0) {
-          keys_of(t, acc, sv[t & 1], kp, MASKED);
-        } else {
-          uint32_t kc[4];
-          keys_of(t, acc, sv[t & 1], kc, MASKED);
+        v4i acc[NT];
 #pragma unroll
-          for (int r = 0; r < 4; r++) best[r] = umin3(best[r], kp[r], kc[r]);
+        for (int k = 0; k < NT; k++) acc[k] = MFMA16(a[k], f, initv[k], 0, 0, 0);
+        const uint32_t Pf = pos_term(t, sv[t & 1], MASKED);
+#pragma unroll
+        for (int k = 0; k < NT; k++) {
+          if constexpr ((t & 1) == 0) {
+            keys_of(acc[k], Pf, kp[k]);
+          } else {
+            uint32_t kc[4];
+            keys_of(acc[k], Pf, kc);
+#pragma unroll
+            for (int r = 0; r < 4; r++) best[k][r] = umin3(best[k][r], kp[k][r], kc[r]);
+          }
         }
       });
     };
@@ -917,27 +957,38 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd8_kernel(SearchArgs p, M
     } else if (full) body(std::false_type{});
     else body(std::true_type{});
 #pragma unroll
-    for (int r = 0; r < 4; r++) {
-      const uint32_t b = best[r];
-      if (b < (1u << 29)) {
-        const int m = 4 * h + r;
-        const uint32_t cost = (b >> 6) - 1u + (uint32_t)(cc[m] & 1);
-        const int dy = y0 + (int)(b & 63u) - (tly0 + 8 * h);
-        const int dx = xn - (tlx0 + 8 * r);
-        const unsigned long long key = ((unsigned long long)cost << 32) |
-                                       ((uint32_t)(dy + 32768) << 16) | (uint32_t)(dx + 32768);
-        atomicMin(&keys[m], key);
+    for (int k = 0; k < NT; k++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const uint32_t b = best[k][r];
+        if (b < (1u << 29)) {
+          const int m = 16 * k + 4 * h + r;
+          const uint32_t cost = (b >> 6) - 1u + (uint32_t)(cc[m] & 1);
+          const int dy = y0 + (int)(b & 63u) - (tly0 + 8 * h);
+          const int dx = xn - (tlx0[k] + 8 * r);
+          const unsigned long long key = ((unsigned long long)cost << 32) |
+                                         ((uint32_t)(dy + 32768) << 16) | (uint32_t)(dx + 32768);
+          atomicMin(&keys[m], key);
+        }
       }
-    }
   }
   }  // groups
   __syncthreads();
-  const int br = tid >> 2, bc = tid & 3;
-  if (tid < 16 && br < nbr && bc < nbc) {
-    const unsigned long long kk = keys[tid];
-    const int out = (br0 + br - p.block_row_begin) * p.nbx + bc0 + bc;
-    store_mv(p.mv, out, kk);
-    if (p.cost) p.cost[out] = (uint32_t)(kk >> 32);
+  const int kt = tid >> 4, br = (tid >> 2) & 3, bc = tid & 3;
+  if (tid < 16 * NT) {
+    int nbck = nbc[0], bc0k = bc0[0];
+#pragma unroll
+    for (int k = 1; k < NT; k++)
+      if (kt == k) {
+        nbck = nbc[k];
+        bc0k = bc0[k];
+      }
+    if (br < nbr && bc < nbck) {
+      const unsigned long long kk = keys[tid];
+      const int out = (br0 + br - p.block_row_begin) * p.nbx + bc0k + bc;
+      store_mv(p.mv, out, kk);
+      if (p.cost) p.cost[out] = (uint32_t)(kk >> 32);
+    }
   }
 }
 
@@ -1934,8 +1985,8 @@ static bool plan_mfma_ssd8(const SearchArgs& p, MfmaGeom* g) {
   g->ngxw = g->ngx;  // one workgroup walks all of a tile's groups
   g->km = ME_SSD8_KM;  // L = 16 km candidate rows per chunk
   const int L = 16 * g->km;
-  // 4 copies + keys + S2 table + the words after each copy granule: 31.8 KB, 5 workgroups per CU
-  g->lds = 4 * (L + 8) * ME_SSD8_WP + 16 * 8 + 16 * 4 + (L + 1) * 256 + (L + 8) * (ME_SSD8_WP / 16) * 4;
+  // 4 copies + keys + S2 table + the words after each copy granule: 31.9 KB (two tiles), 5 workgroups per CU
+  g->lds = 4 * (L + 8) * ME_SSD8_WP + 16 * ME_SSD8_NT * 12 + (L + 1) * 256 + (L + 8) * (ME_SSD8_WP / 16) * 4;
   g->ya0 = max(r0 * 8 - S, 0);
   const int ya1 = min(r1 * 8 + S, H);
   g->rp_rows = ya1 - g->ya0;
@@ -2041,7 +2092,7 @@ hipError_t launch_mfma_ssd(const SearchArgs& p, const MfmaGeom& g, hipStream_t s
   hipError_t e = launch_prep(p, g, jb, stream);
   if (e != hipSuccess) return e;
   if (p.blk == 8) {
-    const dim3 grid8((unsigned)(g.tiles_x * g.tiles_y));
+    const dim3 grid8((unsigned)((g.tiles_x + ME_SSD8_NT - 1) / ME_SSD8_NT * g.tiles_y));
     e = lds_attr((const void*)me_mfma_ssd8_kernel<ME_SSD8_KM>, g.lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(me_mfma_ssd8_kernel<ME_SSD8_KM>, grid8, dim3(256), g.lds, stream, p, g);
