@@ -209,9 +209,22 @@ me_status run_pairs(me_ctx* c, Dev& d, const Job& j, int p0, int p1) {
   // ceil(np / G) + 4, below the ramp's batch count for a large G.)
   const int G = tuning().stream_batch > 0 ? tuning().stream_batch : kPairBatch;
   const size_t region = (size_t)G * nb * 8;  // [G * nb mv (4 B)][G * nb cost (4 B)]
-  size_t nbatches = 0;
-  for (size_t n0 = 0, gb = 1; n0 < np; n0 += gb, gb = std::min<size_t>(gb + std::max<size_t>(1, gb / 2), G))
-    nbatches++;
+  // Batches ramp up 1, 2, 3, 4, 6, 9, then G pairs: the first search starts
+  // after two uploads instead of G + 1.  A batch's new frames upload while the
+  // batch before it searches, and one upload (42 us at 1080p) is 0.6-0.7 of a
+  // pair's search, so batches may grow by about 1.5x: doubling left the GPU
+  // idle 27, 55 and 128 us before the 2-, 4- and 8-pair searches
+  // (profiles/r04m_*).  (Tuning build: ME_STREAM_GROW = growth in tenths.)
+  std::vector<std::pair<int, int>> sched;  // pairs [n0, n1) of each batch
+  {
+    const int grow = tuning().stream_grow > 0 ? tuning().stream_grow : 5;
+    for (int n0 = p0, gb = 1; n0 < p1; n0 += gb, gb = std::min(gb + std::max(1, gb * grow / 10), G)) {
+      if (tuning().stream_ramp == 0) gb = G;  // tuning build: fixed batches (the round-3 behaviour)
+      sched.emplace_back(n0, std::min(p1, n0 + gb));
+    }
+  }
+  const int nsched = (int)sched.size();
+  const size_t nbatches = (size_t)nsched;
   const size_t bneed = region * std::min<size_t>(kEvRing, nbatches);
   if (d.bounce_cap < bneed) {
     if (d.bounce) (void)hipHostFree(d.bounce);
@@ -311,17 +324,6 @@ me_status run_pairs(me_ctx* c, Dev& d, const Job& j, int p0, int p1) {
   int synced = -1;  // newest batch the host has waited for
   std::vector<SearchJob> jobs;
   jobs.reserve((size_t)G);
-  // Batches ramp up 1, 2, 3, 4, 6, then G pairs: the first search starts after
-  // two uploads instead of G + 1.  A batch's new frames upload while the batch
-  // before it searches, and one upload (42 us at 1080p) is 0.6-0.7 of a pair's
-  // search, so batches may grow by about 1.5x: doubling left the GPU idle
-  // 27, 55 and 128 us before the 2-, 4- and 8-pair searches (profiles/r04m_*).
-  std::vector<std::pair<int, int>> sched;  // pairs [n0, n1) of each batch
-  for (int n0 = p0, gb = 1; n0 < p1; n0 += gb, gb = std::min(gb + std::max(1, gb / 2), G)) {
-    if (tuning().stream_ramp == 0) gb = G;  // tuning build: fixed batches (the round-3 behaviour)
-    sched.emplace_back(n0, std::min(p1, n0 + gb));
-  }
-  const int nsched = (int)sched.size();
   // Uploads run one batch ahead of the searches (round 6): batch b + 1's new
   // frames are enqueued on the copy stream together with batch b's search, so
   // by the time batch b + 1's search is enqueued (the host waits for batch

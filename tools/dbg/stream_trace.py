@@ -19,7 +19,7 @@ torch.cuda.synchronize()
 t0 = time.perf_counter()  # clock ramp, as bench.host_stream does (--ramp-ms 100)
 while time.perf_counter() - t0 < 0.1:
     eng.search_pairs(frames, pairs, 16, 32, "sad")
-for rep in range(3):
+for rep in range(int(os.environ.get("REPS", "3"))):  # REPS: more timed calls (outlier hunts)
     t0 = time.perf_counter()
     eng.search_pairs(frames, pairs, 16, 32, "sad")
     dt = time.perf_counter() - t0
