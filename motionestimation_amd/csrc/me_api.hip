@@ -66,7 +66,6 @@ static Tuning read_tuning() {
   env_int("ME_STREAM_RAMP", 0, 1, &t.stream_ramp);
   env_int("ME_STREAM_UPL", 1, 3, &t.stream_upl);
   env_int("ME_STREAM_GROW", 1, 20, &t.stream_grow);
-  env_int("ME_BW_SEGFIRST", 0, 0, &t.bw_seg_first);
   env_int("ME_STREAM_D2H", 0, 1, &t.stream_d2h);
   env_int("ME_STREAM_CPY", 1, 16, &t.stream_cpy);
   env_int("ME_FLOW", 0, 1, &t.flow);

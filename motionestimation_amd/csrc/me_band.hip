@@ -231,11 +231,8 @@ __global__ __launch_bounds__(64 * (NSW + PW), 4) void me_mfma_bw_kernel(SearchAr
     const int j = it.u / g.bw_strips;
     strip = it.u - j * g.bw_strips;
     mfma_job(jb, j, p, g);
-    // (segment 0 may be longer: it walks no bands above its first row)
-    const int first = g.bw_xt || g.bw_seg_first <= 0 ? it.rows : g.bw_seg_first;
-    r0 = g.row0 + (it.seg == 0 ? 0 : first + (it.seg - 1) * it.rows);
-    r1 = !g.bw_xt && it.seg == g.bw_segs - 1 ? g.row0 + g.nrows  // the last: the rest
-                                             : min(r0 + (it.seg == 0 ? first : it.rows), g.row0 + g.nrows);
+    r0 = g.row0 + it.seg * it.rows;
+    r1 = min(r0 + it.rows, g.row0 + g.nrows);
   }
   const int bc0 = strip * C, ncol = min(C, g.nbx - bc0);
   const int tc0 = max(16 * bc0 - S, 0) >> 4;  // first tile column of the strip window
@@ -950,55 +947,38 @@ bool plan_bw(const SearchArgs& p, MfmaGeom* g, int jobs) {
   g->bw_strips = (g->nbx + C - 1) / C;
   // Segments: rounds of resident workgroups x (the most bands one segment
   // walks + ~2 bands of prologue), the smallest.  A segment of rows [r0, r1)
-  // walks bands lo(r0) .. hi(r1 - 1).  The first segment walks no bands above
-  // its rows and the last none below, so they may hold ceil(S/16) more rows
-  // at the same cost: the plan takes a first segment of Lf rows, then L each,
-  // the last the rest, and counts the partial row's search as one more band
-  // of the last segment.  (1080p one frame, 8 segments: even 9-row splits
-  // walk 13 bands in the middle; 10 + 6 x 8 + 9 walk 12.  Round 6's first
-  // uneven try, without the middle shortened, was 1.5 % slower:
-  // profiles/r06g_bw_ab.jsonl.)
+  // walks bands lo(r0) .. hi(r1 - 1); even splits, the last segment the
+  // rest.  (Uneven splits -- a longer first segment, which walks ceil(S/16)
+  // fewer bands, the partial row's segment shorter -- measured 1.5 % slower
+  // at 1080p: profiles/r06g_bw_ab.jsonl; longer first and last segments with
+  // shorter middle ones, 12 bands worst instead of 13 at 1080p one frame,
+  // 1.5 % slower again: 38.6 against 38.0 us per call, r06zl_bw_seg.jsonl.
+  // The segments' band counts do not set the time alone.)
   const int cus = bw_cu_count() * wgs_cu;
   const int nfull = g->row0 + rows;  // (rows from row0: the job's full-height rows)
   auto lo_b = [&](int br) { return std::max(16 * br - S, 0) >> 4; };
   auto hi_b = [&](int br) { return std::min(16 * br + S, p.height - 16) >> 4; };
   const long per = (long)std::max(jobs, 1) * g->bw_strips;
   long best_t = 1L << 40;
-  int best_l = rows, best_segs = 1, best_f = 0;
-  const int hbpen = g->hb_row >= 0 ? 1 : 0;
+  int best_l = rows, best_segs = 1;
   for (int segs = 1; segs <= std::max(1, rows / 4); segs++) {
+    const int L = (rows + segs - 1) / segs;
+    if ((rows + L - 1) / L != segs) continue;  // (an empty last segment)
     const long rounds = (per * segs + cus - 1) / cus;
-    const int L0 = (rows + segs - 1) / segs, ext = (S + 15) / 16 + 1;
-    for (int L = std::max(1, L0 - ext); L <= L0; L++)
-    for (int Lf = L0; Lf <= std::min(rows, L0 + ext); Lf++) {
-      // the first Lf rows, then L each, the last the rest (1 .. L + ext rows)
-      const int last = segs > 1 ? rows - Lf - (segs - 2) * L : 0;
-      if (segs == 1 ? (Lf != rows || L != L0) : (last < 1 || last > L + ext)) continue;
-#ifdef ME_BW_SEG_UNIFORM
-      if (Lf != L0 || L != L0) continue;  // A/B build: round 6's uniform splits only
-#endif
-      int worst = 0;  // bands of the longest segment
-      for (int k = 0, r0 = g->row0; k < segs; k++) {
-        const int r1 = k == segs - 1 ? nfull : std::min(r0 + (k == 0 ? Lf : L), nfull);
-        worst = std::max(worst, hi_b(r1 - 1) - lo_b(r0) + 1 + (k == segs - 1 ? hbpen : 0));
-        r0 = r1;
-      }
-      const long t = rounds * (worst + 2);
-      if (t < best_t || (t == best_t && Lf == L && L == L0)) {  // (ties: the uniform split)
-        best_t = t;
-        best_l = L;
-        best_segs = segs;
-        best_f = Lf == L ? 0 : Lf;
-      }
+    int worst = 0;  // bands of the longest segment
+    for (int r0 = g->row0; r0 < nfull; r0 += L)
+      worst = std::max(worst, hi_b(std::min(r0 + L, nfull) - 1) - lo_b(r0) + 1);
+    const long t = rounds * (worst + 2);
+    if (t < best_t) {
+      best_t = t;
+      best_l = L;
+      best_segs = segs;
     }
   }
   if (tuning().bw_seg > 0) {
     best_l = std::min(rows, tuning().bw_seg);
     best_segs = (rows + best_l - 1) / best_l;
-    best_f = 0;
   }
-  if (tuning().bw_seg_first == 0) best_f = 0;  // tuning build: uniform splits
-  g->bw_seg_first = best_f;
   g->bw_seg_rows = best_l;
   g->bw_abl = tuning().bw_abl;
   g->bw_segs = best_segs;
@@ -1009,7 +989,6 @@ bool plan_bw(const SearchArgs& p, MfmaGeom* g, int jobs) {
     g->bw_xt = 1;
     g->bw_seg_rows = rows;
     g->bw_segs = 1;
-    g->bw_seg_first = 0;
   }
   g->lds = bw_lds_bytes(lp, pp, ns, nsw);
   if (g->lds > 160 * 1024 / wgs_cu) return false;

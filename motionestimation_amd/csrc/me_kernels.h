@@ -179,7 +179,6 @@ struct MfmaGeom {
   int bw_strips;         // strips per job
   int bw_seg_rows;       // block rows per workgroup (segment)
   int bw_segs;           // segments per job
-  int bw_seg_first;      // block rows of segment 0 when it differs from bw_seg_rows (0: uniform)
   int bw_xt;             // per-XCD tail split (bw_cx CUs per XCD): workgroup decode in bw_item()
   int bw_cx;
   int bw_lp, bw_pp;      // window row pitch (bytes), P0 plane row pitch (ints)

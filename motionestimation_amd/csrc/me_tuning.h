@@ -26,7 +26,6 @@ struct Tuning {
   int stream_d2h = 0;     // ME_STREAM_D2H=1: pair records download on a stream of their own
   int stream_cpy = 0;     // ME_STREAM_CPY=1..16: threads of a pageable frame's staging copy (0 = 4)
   int stream_ramp = -1;   // ME_STREAM_RAMP=0: no ramp, every launch ME_STREAM_BATCH pairs (-1 = ramp)
-  int bw_seg_first = -1;  // ME_BW_SEGFIRST=0: band-walk segments split uniformly (-1 = longer first segment allowed)
   int stream_grow = 0;    // ME_STREAM_GROW=1..20: ramp growth per batch in tenths (0 = 5: 1.5x)
   int stream_upl = 0;     // ME_STREAM_UPL=1..3: batches the uploads run ahead of the searches (0 = 1)
   int flow = -1;          // ME_FLOW=0|1: SAD flow kernel off / allowed (-1 = automatic)
