@@ -75,3 +75,18 @@ def test_frames_per_launch_pricing():
     assert bench.sad_frames_per_launch(7680, 4320, 8, 128, 16) == 16
     assert bench.sad_frames_per_launch(7680, 68 * 8, 8, 128, 16) == 16
     assert bench.ssd_frames_per_launch(7680, 4320, 8, 128, 16) == 1
+
+
+def test_committed_pmc_summary_feeds_the_roofline_figures():
+    """bench.py reads its `traffic` and the 8x8 SSD line's `valu` figure from
+    the committed profiles/pmc_summary.json (tools/profile.sh): the entries the
+    default and 8K SSD lines need exist, and the VALU pass counts more VALU
+    than MFMA wave-instructions (SQ_INSTS_VALU includes the MFMAs)."""
+    sys.path.insert(0, REPO)
+    import bench
+    t, ts = bench.load_traffic("1080p_b16_s32_sad_f16")
+    assert t and ts and t > 60e6
+    v = bench.load_valu("8k_b8_s128_ssd_f16")
+    assert v is not None and v["kernel"].startswith("me_mfma_ssd8_kernel")
+    assert v["valu"] > v["mfma"] > 0
+    assert bench.load_valu("no_such_workload") is None
