@@ -207,7 +207,13 @@ me_status run_pairs(me_ctx* c, Dev& d, const Job& j, int p0, int p1) {
   // is free again when its batch index comes round: at most kEvRing * G
   // pairs pinned, whatever the length of the pair list.  (Round 5 sized it
   // ceil(np / G) + 4, below the ramp's batch count for a large G.)
-  const int G = tuning().stream_batch > 0 ? tuning().stream_batch : kPairBatch;
+  bool all_pinned = true;
+  for (int n = p0; n < p1 && all_pinned; n++)
+    for (int side = 0; side < 2; side++)
+      all_pinned = all_pinned &&
+                   host_range_pinned(j.frames[j.pairs[2 * n + side]], (size_t)(H - 1) * j.stride + W);
+  // pinned frames: 12 pairs per launch (one-ahead uploads); pageable: round 5's 8
+  const int G = tuning().stream_batch > 0 ? tuning().stream_batch : all_pinned ? kPairBatch : 8;
   const size_t region = (size_t)G * nb * 8;  // [G * nb mv (4 B)][G * nb cost (4 B)]
   // Batches ramp up 1, 2, 3, 4, 6, 9, then G pairs: the first search starts
   // after two uploads instead of G + 1.  A batch's new frames upload while the
@@ -295,11 +301,6 @@ me_status run_pairs(me_ctx* c, Dev& d, const Job& j, int p0, int p1) {
   // 9.5k, 4 ahead 9.4k / 9.0k.  Pinned frames need the host only to enqueue a
   // pair (~25 us); pageable ones also to copy them into staging, so they get
   // one more pair of slack.
-  bool all_pinned = true;
-  for (int n = p0; n < p1 && all_pinned; n++)
-    for (int side = 0; side < 2; side++)
-      all_pinned = all_pinned &&
-                   host_range_pinned(j.frames[j.pairs[2 * n + side]], (size_t)(H - 1) * j.stride + W);
   const int env_ahead = tuning().stream_ahead;  // tuning build: 1..8, 9 unbounded (diagnostic)
   const int kAhead = env_ahead > 8 ? 1 << 30 : env_ahead >= 1 ? env_ahead : (all_pinned ? 2 : 3);
   // Pairs are searched G at a time in one job-table launch (launch_jobs: the
@@ -312,7 +313,12 @@ me_status run_pairs(me_ctx* c, Dev& d, const Job& j, int p0, int p1) {
   // 2 G + 1 (with G + 1, most reused slots were batch b - 1's, and the copy
   // queue waited for that search before uploading).
   // (tuning build: ME_STREAM_UPL = U batches ahead needs (U + 1) G + 1)
-  const int U = tuning().stream_upl > 0 ? tuning().stream_upl : 1;
+  // Pageable frames keep round 5's order (a batch's uploads just before its
+  // search, U = 0) and 8 pairs per launch: their rate is bound by the host's
+  // staging copies, and one-ahead uploads gained nothing there (paired runs,
+  // four rounds: 11.6-12.8k one ahead, 11.7-13.0k this way, 11.0-12.6k round
+  // 5's code; profiles/r06zn_stream_ab.jsonl).
+  const int U = tuning().stream_upl > 0 ? tuning().stream_upl : all_pinned ? 1 : 0;
   const size_t cool = (size_t)std::max(cooling_slots(), (U + 1) * G + 1);
   // Ordering events: one per batch on each stream, not one per frame slot.
   // The round-3 scheme (a ready event per upload, a free event per released
@@ -442,6 +448,7 @@ me_status run_pairs(me_ctx* c, Dev& d, const Job& j, int p0, int p1) {
       HIPCHK(c, hipEventSynchronize(d.batch_ev[(batch - kAhead) % kEvRing]));
       synced = batch - kAhead;
     }
+    if (U == 0 && (s = upload_batch(batch)) != ME_OK) return s;
     if (batch == 0)
       for (int u = 0; u < U && u < nsched; u++)
         if ((s = upload_batch(u)) != ME_OK) return s;
@@ -470,7 +477,7 @@ me_status run_pairs(me_ctx* c, Dev& d, const Job& j, int p0, int p1) {
     // then the next batch's uploads (after the launch: pageable frames' host
     // copies into staging must not hold back this search's enqueue), then the
     // previous batch's records behind them on the copy stream
-    if (batch + U < nsched && (s = upload_batch(batch + U)) != ME_OK) return s;
+    if (U > 0 && batch + U < nsched && (s = upload_batch(batch + U)) != ME_OK) return s;
     while (!own_dl && downloaded < batch)
       if ((s = download()) != ME_OK) return s;
     if (own_dl && (s = download()) != ME_OK) return s;
