@@ -8,11 +8,12 @@
 //   - each frame is uploaded once per device, into a device slot that lives
 //     from the first to the last pair reading it;
 //   - pairs are searched in job-table launches (launch_jobs) ramping 1, 2, 3,
-//     4, 6, 9 and then 12 pairs: a launch's fill and drain are paid once per
-//     batch, and the first search starts after two uploads (profiles/r04h_*);
-//   - uploads run one batch ahead of the searches, and a batch's frames that
-//     are adjacent in host memory and in their device slots go up in one
-//     copy (round 6);
+//     4, 6, 9 and then 12 pairs (pageable frames: 1, 2, 3, 4, 6, then 8): a
+//     launch's fill and drain are paid once per batch, and the first search
+//     starts after two uploads (profiles/r04h_*);
+//   - pinned frames upload one batch ahead of the searches, and a batch's
+//     frames that are adjacent in host memory and in their device slots go up
+//     in one copy (round 6);
 //   - uploads run on a copy stream, searches on the compute stream; the
 //     host-side staging and upload of pair n+1's new frame overlap the search
 //     of pair n (slots are reused oldest-freed first, so an upload never
