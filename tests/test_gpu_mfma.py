@@ -475,3 +475,23 @@ def test_batched_ssd_partial_right_column_stays_on_mfma(engine, ssd_path):
         omv, oc, _ = O.full_search(r, c, 16, span, "ssd", threads=NT)
         np.testing.assert_array_equal(mv[f], omv, err_msg=f"frame {f}")
         np.testing.assert_array_equal(co[f], oc, err_msg=f"frame {f}")
+
+
+def test_mfma8_two_tile_workgroups_random_shapes(engine):
+    """Round 6: the 8x8 kernel runs two horizontally adjacent 4x4-block tiles
+    per workgroup over the union of their candidate columns.  Random widths
+    give odd tile counts (the last workgroup's second tile absent), partial
+    tiles (nbx % 4 != 0); ranges reach past either
+    tile's own columns; every field against the oracle, and the 8x8 MFMA
+    kernel must be the one that ran."""
+    rng = np.random.default_rng(6262)
+    for case in range(12):
+        # whole 8x8 blocks (a partial row or column would run the generic
+        # kernel after the MFMA one and be the path reported)
+        w = 8 * int(rng.integers(5, 45))           # nbx 5 .. 44: tiles_x odd and even
+        h = 8 * int(rng.integers(3, 18))
+        span = int(rng.choice([3, 9, 16, 31, 47, 64, 100, 128]))
+        ref, cur = _pair(rng, h, w, dx=int(rng.integers(-6, 7)), dy=int(rng.integers(-6, 7)))
+        tag = f"case {case}: {w}x{h} S{span} tiles_x {((w // 8) + 3) // 4}"
+        _check8(engine, ref, cur, span, tag)
+        assert engine.last_search_path() == "mfma_8x8", (tag, engine.last_search_path())
