@@ -63,6 +63,9 @@ constexpr int MFMA_DLY = 1;
 #ifndef ME_SSD8_ABL
 #define ME_SSD8_ABL 0  // A/B ablations of the 8x8 kernel (1: no steps, 2: no re-staging); 0 in the product
 #endif
+#ifndef ME_SSD8_WPE
+#define ME_SSD8_WPE 4  // 8x8: waves per SIMD the register budget targets (<= 128 VGPRs)
+#endif
 #ifndef ME_SSD8_NT
 #define ME_SSD8_NT 2  // 8x8: horizontally adjacent 4x4-block tiles per workgroup (1 or 2)
 #endif
@@ -663,7 +666,7 @@ __attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd16_kernel(SearchArgs p, 
 // candidate ranges overlap in all but 32 columns.
 template <int KM8>
 __global__ __launch_bounds__(256)
-__attribute__((amdgpu_waves_per_eu(4))) void me_mfma_ssd8_kernel(SearchArgs p, MfmaGeom g) {
+__attribute__((amdgpu_waves_per_eu(ME_SSD8_WPE))) void me_mfma_ssd8_kernel(SearchArgs p, MfmaGeom g) {
   constexpr int WP = ME_SSD8_WP;   // bytes per copy row (64 positions + 7 + align, 16-byte granules)
   constexpr int L = 16 * KM8;      // candidate rows per chunk (yidx < 64)
   constexpr int CROWS = L + 8;     // rows y0 .. y0 + L + 6, + the last (unused) prefetch
