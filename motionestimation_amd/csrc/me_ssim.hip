@@ -290,49 +290,6 @@ __device__ __forceinline__ void stats_w16(const uint32_t* t, int pr, int c, int 
   *v = __fdiv_rn(acc, nf);
 }
 
-// stats_at<16> for the positions at rows pr and pr + 1 of column c at once:
-// the same operations per position, in the same order, two positions per
-// packed fp32 instruction (v_pk_add_f32 / v_pk_mul_f32, each lane-half
-// rounded as the scalar instruction), the 17 staged rows' words aligned once.
-__device__ __forceinline__ void stats16_pair(const uint32_t* t, int pr, int c, float2* m,
-                                             float2* v) {
-  typedef float f2v __attribute__((ext_vector_type(2)));
-  const int a = c & 3, wb = c >> 2;
-  uint32_t w[17][4];
-#pragma unroll
-  for (int i = 0; i < 17; i++) {
-    const uint32_t* row = t + (pr + i) * STATS_TW + wb;
-    uint32_t d[5];
-#pragma unroll
-    for (int e = 0; e < 5; e++) d[e] = row[e];
-#pragma unroll
-    for (int q = 0; q < 4; q++) w[i][q] = __builtin_amdgcn_alignbyte(d[q + 1], d[q], (uint32_t)a);
-  }
-  uint32_t sa = 0, sb = 0;
-#pragma unroll
-  for (int i = 0; i < 16; i++)
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-      sa = __builtin_amdgcn_sad_u8(w[i][q], 0u, sa);
-      sb = __builtin_amdgcn_sad_u8(w[i + 1][q], 0u, sb);
-    }
-  // sums / 256: exact, as __fdiv_rn(s, 256.f)
-  const f2v mf = {__fmul_rn((float)sa, 1.0f / 256.0f), __fmul_rn((float)sb, 1.0f / 256.0f)};
-  f2v acc = {0.f, 0.f};
-#pragma unroll
-  for (int i = 0; i < 16; i++)
-#pragma unroll
-    for (int q = 0; q < 4; q++)
-#pragma unroll
-      for (int b = 0; b < 4; b++) {
-        const f2v x = {(float)((w[i][q] >> (8 * b)) & 255u), (float)((w[i + 1][q] >> (8 * b)) & 255u)};
-        const f2v d = x - mf;
-        acc = acc + d * d;
-      }
-  *m = make_float2(mf.x, mf.y);
-  *v = make_float2(__fmul_rn(acc.x, 1.0f / 256.0f), __fmul_rn(acc.y, 1.0f / 256.0f));
-}
-
 // One launch for every statistic the search reads: grid rows [0, gy[0]) the
 // current blocks' (mean, stddev, byte sum) for the matrix-core kernel, then
 // gy[1] rows of tiles of plane 1 (the full rows'), gy[2] of plane 2 (the
@@ -414,10 +371,8 @@ __global__ __launch_bounds__(256) void me_ssim_stats_kernel(SearchArgs p, SsimSt
                 ? p.ref[(ptrdiff_t)(y - p.ref_row0) * p.stride + xx] : 0;
   }
   __syncthreads();
-  const int c = tid & 63, g = tid >> 6, x = x0 + c;
-  if (x >= s.pitch) return;
   const float nfp = (float)(B * ph);
-  auto put = [&](int rr, float m, float v) {
+  auto put = [&](int rr, int x, float m, float v) {
     const size_t e = (size_t)rr * s.ld + x;
     if (s.compact) {
       float* sd = reinterpret_cast<float*>(plane);
@@ -429,17 +384,70 @@ __global__ __launch_bounds__(256) void me_ssim_stats_kernel(SearchArgs p, SsimSt
     }
   };
   if (B == 16 && ph == 16) {
+    // 16 x 16 patches (the full rows' plane): the staged bytes once more as
+    // float pairs (column j, column j + 32) of each row, and 16-row column
+    // sums.  Thread (cc, rg) then runs the positions (cc, cc + 32) of rows
+    // 2 rg and 2 rg + 1: per pixel one aligned 8-byte LDS read feeds one
+    // packed chain step of two positions (v_pk_add / v_pk_mul, each half
+    // rounded as the scalar op, in patch_stats' raster order), and the two
+    // rows' chains interleave.  (Bytes converted per read with two positions
+    // per chain, round 6's first form: 57.4 against 52.2 us at 1080p,
+    // profiles/r06zv_*.)
+    typedef float f2v_ __attribute__((ext_vector_type(2)));
+    __shared__ f2v_ pf[31 * 47];
+    __shared__ int cs[16 * 79];
+    constexpr int TB = STATS_TW * 4;  // staged bytes per row
+    for (int i = tid; i < 31 * 47; i += 256) {
+      const int r = i / 47, j = i - r * 47;
+      pf[i] = f2v_{(float)tb[r * TB + j], (float)tb[r * TB + j + 32]};
+    }
+    for (int i = tid; i < 16 * 79; i += 256) {
+      const int r = i / 79, col = i - r * 79;
+      int sum = 0;
+#pragma unroll
+      for (int q = 0; q < 16; q++) sum += tb[(r + q) * TB + col];
+      cs[i] = sum;
+    }
+    __syncthreads();
+    const int cc = tid & 31, rg = tid >> 5, r0 = 2 * rg;
+    f2v_ mf[2];
+#pragma unroll
+    for (int rw = 0; rw < 2; rw++) {
+      int sa = 0, sb = 0;
+#pragma unroll
+      for (int k = 0; k < 16; k++) {
+        sa += cs[(r0 + rw) * 79 + cc + k];
+        sb += cs[(r0 + rw) * 79 + cc + 32 + k];
+      }
+      // byte sums / 256: exact, as __fdiv_rn(s, 256.f)
+      mf[rw] = f2v_{__fmul_rn((float)sa, 1.0f / 256.0f), __fmul_rn((float)sb, 1.0f / 256.0f)};
+    }
+    f2v_ acc[2] = {f2v_{0.f, 0.f}, f2v_{0.f, 0.f}};
 #pragma unroll 1
-    for (int j = 0; j < 4; j += 2) {
-      const int pr = 4 * g + j, rr = y0 + pr;
-      if (rr >= s.rows) break;
-      float2 m, v;
-      stats16_pair(t, pr, c, &m, &v);  // row pr + 1 + 15 <= 30: staged
-      put(rr, m.x, v.x);
-      if (rr + 1 < s.rows) put(rr + 1, m.y, v.y);
+    for (int i = 0; i < 16; i++) {
+      const f2v_* ra = pf + (r0 + i) * 47 + cc;
+      const f2v_* rb = ra + 47;
+#pragma unroll
+      for (int k = 0; k < 16; k++) {
+        const f2v_ da = ra[k] - mf[0], db = rb[k] - mf[1];
+        acc[0] = acc[0] + da * da;
+        acc[1] = acc[1] + db * db;
+      }
+    }
+#pragma unroll
+    for (int rw = 0; rw < 2; rw++) {
+      const int rr = y0 + r0 + rw;
+      if (rr >= s.rows) continue;
+#pragma unroll
+      for (int hh = 0; hh < 2; hh++) {
+        const int x = x0 + cc + 32 * hh;
+        if (x < s.pitch) put(rr, x, mf[rw][hh], __fmul_rn(acc[rw][hh], 1.0f / 256.0f));
+      }
     }
     return;
   }
+  const int c = tid & 63, g = tid >> 6, x = x0 + c;
+  if (x >= s.pitch) return;
 #pragma unroll 1
   for (int j = 0; j < 4; j++) {
     const int pr = 4 * g + j, rr = y0 + pr;
@@ -453,7 +461,7 @@ __global__ __launch_bounds__(256) void me_ssim_stats_kernel(SearchArgs p, SsimSt
         case 8: stats_at<8>(t, pr, c, B, &m, &v); break;
         default: stats_at<0>(t, pr, c, B, &m, &v); break;
       }
-    put(rr, m, v);
+    put(rr, x, m, v);
   }
 }
 
