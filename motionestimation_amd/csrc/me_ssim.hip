@@ -292,8 +292,8 @@ __device__ __forceinline__ void stats_w16(const uint32_t* t, int pr, int c, int 
 
 // One launch for every statistic the search reads: grid rows [0, gy[0]) the
 // current blocks' (mean, stddev, byte sum) for the matrix-core kernel, then
-// gy[1] rows of tiles of plane 1 (the full rows'), gy[2] of plane 2 (the
-// partial bottom row's, patch height ph[2] < 16).
+// gy[2] rows of tiles of plane 2 (the partial bottom row's, patch height
+// ph[2] < 16), then gy[1] of plane 1 (the full rows').
 struct SsimStatsJob {
   SsimPlane pl[3];
   float2* out[3];
@@ -348,8 +348,18 @@ __global__ __launch_bounds__(256) void me_ssim_stats_kernel(SearchArgs p, SsimSt
   __shared__ uint32_t t[STATS_TR * STATS_TW];
   const int B = p.blk;
   const int tid = (int)threadIdx.x;
-  int yb = (int)blockIdx.y, k = 0;
-  while (k < 2 && yb >= J.gy[k]) yb -= J.gy[k++];
+  // grid rows: the current blocks' statistics, then the partial row's plane
+  // (its workgroups run the longest scalar chains: first, not as a tail),
+  // then the full rows' plane
+  int yb = (int)blockIdx.y, k;
+  if (yb < J.gy[0]) {
+    k = 0;
+  } else if ((yb -= J.gy[0]) < J.gy[2]) {
+    k = 2;
+  } else {
+    yb -= J.gy[2];
+    k = 1;
+  }
   if (k == 0) {
     const int e = (yb * (int)gridDim.x + (int)blockIdx.x) * 256 + tid;
     if (e < J.cst_n)
